@@ -1,0 +1,212 @@
+/*
+ * rl_engine.h — C-ABI of the MI355X batched rate-limit decision engine.
+ *
+ * This is the drop-in boundary that replaces the reference's
+ * algorithm + storage pair beneath its unchanged Java `RateLimiter` interface:
+ *
+ *   reference interface                                  replaced by
+ *   ---------------------------------------------------  -----------------------------
+ *   RateLimiter.tryAcquire(String)                        rl_try_acquire_batch (permits=1)
+ *     core/RateLimiter.java:16
+ *   RateLimiter.tryAcquire(String,int)                    rl_try_acquire_batch
+ *     core/RateLimiter.java:26
+ *     algorithms/SlidingWindowRateLimiter.java:85-131
+ *     algorithms/TokenBucketRateLimiter.java:105-143 (+ Lua :38-68)
+ *   RateLimiter.getAvailablePermits(String)               rl_available
+ *     core/RateLimiter.java:35, SlidingWindowRateLimiter.java:133-137,
+ *     TokenBucketRateLimiter.java:145-151
+ *   RateLimiter.reset(String)                             rl_reset
+ *     core/RateLimiter.java:43, SlidingWindowRateLimiter.java:139-153,
+ *     TokenBucketRateLimiter.java:153-158
+ *   new SlidingWindowRateLimiter(storage, config, reg)    rl_add_limiter(RL_ALGO_SLIDING_WINDOW, ...)
+ *     SlidingWindowRateLimiter.java:46-78
+ *   new TokenBucketRateLimiter(storage, config, reg)      rl_add_limiter(RL_ALGO_TOKEN_BUCKET, ...)
+ *     TokenBucketRateLimiter.java:70-97
+ *   RateLimitConfig.validate()                            rl_add_limiter argument checks
+ *     core/RateLimitConfig.java:46-56
+ *   RedisRateLimitStorage (JedisPool, Redis keyspace)     rl_create / rl_destroy (HBM state table)
+ *     storage/RedisRateLimitStorage.java:22-35
+ *
+ * Everything is plain C: pointers + sizes, no C++ types, no exceptions. Every
+ * entry point returns an int status (RL_OK = 0, < 0 on error). The JNI / FFM
+ * bindings that a Java maintainer adds on top are shown in INTEGRATION.md.
+ *
+ * Semantics (bit-exact with the reference):
+ *  - key_hash is the caller's 64-bit hash of the String key (hashing happens on
+ *    the JVM side). State is kept per (limiter id, key_hash).
+ *  - now_ns is converted to milliseconds as floorDiv(now_ns, 1e6); the reference
+ *    reads System.currentTimeMillis().
+ *  - Requests of one batch are applied in array (arrival) order per key.
+ *    Sliding-window state requires per-key non-decreasing now_ms (in-order
+ *    replay of a wall-clock trace); token-bucket state has no such requirement.
+ *  - A denied request never changes state (SlidingWindowRateLimiter.java:104-111,
+ *    TokenBucketRateLimiter.java:61-67,110-116).
+ */
+#ifndef RL_ENGINE_H
+#define RL_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RL_ABI_VERSION 1
+
+/* ---- status codes -------------------------------------------------------- */
+#define RL_OK                   0
+#define RL_E_INVALID_ARG      (-1)  /* bad argument to an entry point; IllegalArgumentException on the Java side */
+#define RL_E_INVALID_REQUEST  (-2)  /* >=1 request had permits <= 0 or an unknown limiter id (others were applied) */
+#define RL_E_CAPACITY         (-3)  /* a state-table region overflowed; affected requests report RL_REMAINING_ERROR */
+#define RL_E_DEVICE           (-4)  /* HIP runtime / device failure; StorageException on the Java side */
+#define RL_E_NOMEM            (-5)  /* device or host allocation failed */
+#define RL_E_TOO_LARGE        (-6)  /* batch larger than rl_opts.max_batch */
+#define RL_E_LIMITERS         (-7)  /* too many limiters / table space exhausted */
+
+/* ---- algorithms ---------------------------------------------------------- */
+#define RL_ALGO_SLIDING_WINDOW 0    /* algorithms/SlidingWindowRateLimiter.java */
+#define RL_ALGO_TOKEN_BUCKET   1    /* algorithms/TokenBucketRateLimiter.java   */
+
+/* ---- per-request operation (rl_execute_batch) ----------------------------- */
+#define RL_OP_ACQUIRE 0             /* tryAcquire(key, permits)     */
+#define RL_OP_PEEK    1             /* getAvailablePermits(key)     */
+#define RL_OP_RESET   2             /* reset(key)                   */
+
+/* ---- sentinel values of `remaining` --------------------------------------- */
+#define RL_REMAINING_UNKNOWN  (-1)  /* TB permits > maxPermits: "unable to determine" (RateLimiter.java:33) */
+#define RL_REMAINING_INVALID  (-2)  /* permits <= 0 or unknown limiter (IllegalArgumentException in Java)   */
+#define RL_REMAINING_ERROR    (-3)  /* request not applied: state-table region full (RL_E_CAPACITY)         */
+
+/* ---- limits of this implementation (checked by rl_add_limiter) ------------ */
+#define RL_MAX_LIMITERS         255
+#define RL_SW_MAX_PERMITS_LIMIT 2147483646LL        /* SW counts kept as u32 */
+#define RL_TB_MAX_PERMITS_LIMIT 9007199254740992LL  /* 2^53: Lua numbers are IEEE doubles */
+#define RL_MAX_WINDOW_MS        1073741823LL        /* ~12.4 days; bucket offsets kept as i32 */
+
+typedef struct rl_engine rl_engine;
+
+typedef struct rl_opts {
+    int32_t  device;            /* HIP device ordinal (-1: current device)                  */
+    uint32_t flags;             /* RL_OPT_* bits                                            */
+    uint64_t max_batch;         /* largest n accepted by the batch entry points             */
+    uint64_t default_capacity;  /* expected live keys per limiter when rl_add_limiter is used */
+    uint32_t shard_index;       /* multi-GPU: this engine owns keys with owner(h) == shard   */
+    uint32_t shard_count;       /* multi-GPU: number of shards (power of two, 1 = no sharding) */
+} rl_opts;
+
+#define RL_OPT_STAGE_TIMING 0x1u  /* record hipEvents around every stage (rl_stage_times) */
+
+typedef struct rl_limiter_config {
+    int32_t  algo;              /* RL_ALGO_*                                                  */
+    int32_t  reserved;
+    int64_t  max_permits;       /* RateLimitConfig.maxPermits (RateLimitConfig.java:19)       */
+    int64_t  window_ms;         /* RateLimitConfig.window.toMillis() (RateLimitConfig.java:24) */
+    double   refill_per_s;      /* RateLimitConfig.refillRate (RateLimitConfig.java:31); TB only */
+    uint64_t capacity;          /* expected live keys (table sizing); 0 = rl_opts.default_capacity */
+} rl_limiter_config;
+
+typedef struct rl_batch_stats {
+    uint64_t n;                 /* requests in the last batch                                 */
+    uint64_t allowed;           /* requests allowed                                           */
+    uint64_t distinct_keys;     /* U: distinct (limiter, key) touched (for the roofline)      */
+    uint64_t invalid;           /* requests rejected as invalid                               */
+    uint64_t capacity_errors;   /* requests not applied because a region was full            */
+    uint64_t regions_touched;   /* state-table regions loaded + written back                  */
+    uint64_t table_bytes;       /* bytes of state-table regions moved (load + write-back)     */
+} rl_batch_stats;
+
+/* Create / destroy an engine on one GPU. Replaces the JedisPool + Redis keyspace
+ * (RedisRateLimitStorage.java:22-35). */
+int  rl_create(const rl_opts* opts, rl_engine** out);
+void rl_destroy(rl_engine* e);
+
+/* Register a limiter; mirrors the constructors SlidingWindowRateLimiter.java:46-78 /
+ * TokenBucketRateLimiter.java:70-97 (config.validate() + refillRate > 0 for TB).
+ * The id is the `limiter` value used in the batch calls. */
+int  rl_add_limiter(rl_engine* e, int algo, int64_t max_permits, int64_t window_ms,
+                    double refill_per_s, uint16_t* id);
+int  rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* cfg, uint16_t* id);
+
+/* tryAcquire over a batch of HOST buffers (pageable or pinned).
+ *   allowed[i]      1 if request i acquired its permits
+ *   remaining[i]    SW: max(0, max - estimate) at now_i after applying request i
+ *                   TB: (long) token balance returned by the Lua script, -1 if permits > max
+ *   tokens_after[i] TB: the fp64 balance returned by the script (NaN otherwise); may be NULL
+ * `limiter` may be NULL (all requests use limiter 0). Returns RL_E_INVALID_REQUEST if
+ * any request was invalid (those report RL_REMAINING_INVALID; the rest are applied). */
+int  rl_try_acquire_batch(rl_engine* e, size_t n,
+                          const uint64_t* key_hash, const int32_t* permits,
+                          const int64_t* now_ns, const uint16_t* limiter,
+                          uint8_t* allowed, int64_t* remaining, double* tokens_after);
+
+/* Mixed operations (RL_OP_*) over host buffers; `op` may be NULL (all ACQUIRE). */
+int  rl_execute_batch(rl_engine* e, size_t n,
+                      const uint64_t* key_hash, const int32_t* permits,
+                      const int64_t* now_ns, const uint16_t* limiter, const uint8_t* op,
+                      uint8_t* allowed, int64_t* remaining, double* tokens_after);
+
+/* Same as rl_execute_batch on DEVICE-resident buffers, enqueued on `stream`
+ * (a hipStream_t; NULL = the engine's stream). Asynchronous: results are ready
+ * when the stream completes; the status of the batch is then available from
+ * rl_last_status(). Used by bench.py and the multi-GPU router (HBM-resident data). */
+int  rl_execute_batch_device(rl_engine* e, size_t n,
+                             const uint64_t* key_hash, const int32_t* permits,
+                             const int64_t* now_ns, const uint16_t* limiter, const uint8_t* op,
+                             uint8_t* allowed, int64_t* remaining, double* tokens_after,
+                             void* stream);
+int  rl_last_status(rl_engine* e);     /* synchronises the engine stream */
+
+/* getAvailablePermits for n keys at now_ns[i] (host buffers). SW: max(0, max - estimate).
+ * TB: (long) min(cap, tokens + elapsed*rate) without consuming (the reference's TB
+ * getAvailablePermits is broken). */
+int  rl_available(rl_engine* e, uint16_t limiter, size_t n, const uint64_t* key_hash,
+                  const int64_t* now_ns, int64_t* available);
+
+/* reset(key) for n keys at now_ns[i]: SW deletes the current and previous window
+ * buckets; TB deletes the bucket. */
+int  rl_reset(rl_engine* e, uint16_t limiter, size_t n, const uint64_t* key_hash,
+              const int64_t* now_ns);
+
+/* Observability. */
+int  rl_batch_stats_get(rl_engine* e, rl_batch_stats* out);
+/* Milliseconds of each pipeline stage of the last batch (needs RL_OPT_STAGE_TIMING);
+ * names[i] are static strings. Returns the number of stages written (<= cap). */
+int  rl_stage_times(rl_engine* e, const char** names, float* ms, int cap);
+int  rl_sync(rl_engine* e);
+const char* rl_strerror(int status);
+int  rl_abi_version(void);
+
+/* ---- multi-GPU routing helpers (device buffers, engine stream) ------------
+ * owner(key_hash) is the shard that holds the key's state. rl_route_partition
+ * stably partitions a batch by owner: perm[j] = source index of the j-th request
+ * in owner order, counts[s] = requests for shard s (host array of shard_count). */
+uint32_t rl_owner_of(uint64_t key_hash, uint16_t limiter, uint32_t shard_count);
+int  rl_route_partition(rl_engine* e, size_t n, const uint64_t* key_hash,
+                        const uint16_t* limiter, uint32_t shard_count,
+                        uint32_t* perm, uint64_t* counts_host, void* stream);
+
+/* ---- synthetic traces (bench / tests; deterministic in (seed, index)) ------ */
+#define RL_DIST_UNIFORM 0
+#define RL_DIST_ZIPF    1
+typedef struct rl_trace_spec {
+    uint64_t seed;
+    uint64_t n_keys;            /* key population                                */
+    int32_t  dist;              /* RL_DIST_*                                      */
+    int32_t  permits_max;       /* permits uniform in [1, permits_max]            */
+    double   zipf_s;            /* Zipf exponent (dist = RL_DIST_ZIPF)            */
+    int64_t  t0_ns;             /* first arrival                                  */
+    int64_t  span_ns;           /* arrivals evenly spaced over [t0, t0 + span)    */
+    uint64_t index_base;        /* global index of element 0 (sharded traces)     */
+    uint64_t n_total;           /* total length of the global trace (time axis)  */
+    uint16_t n_limiters;        /* limiter ids assigned round-robin by key rank   */
+    uint16_t reserved[3];
+} rl_trace_spec;
+int  rl_synth_trace_device(rl_engine* e, const rl_trace_spec* spec, size_t n,
+                           uint64_t* key_hash, int32_t* permits, int64_t* now_ns,
+                           uint16_t* limiter, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RL_ENGINE_H */
