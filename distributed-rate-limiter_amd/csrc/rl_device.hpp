@@ -1,0 +1,323 @@
+// rl_device.hpp — device-side layout, record codecs and the exact per-request
+// semantics of the two reference algorithms, for gfx950 (MI355X).
+//
+// Everything here is compiled with -ffp-contract=off (see Makefile) and also
+// carries `#pragma clang fp contract(off)`: Java (SlidingWindowRateLimiter.java:174)
+// and Lua (TokenBucketRateLimiter.java:56-58) round every multiply and every add
+// separately; hipcc would otherwise fuse `a + b*c` into v_fmac_f64 and flip
+// decisions at thresholds (tests/golden "fmaFlip*").
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rl {
+
+// ---------------------------------------------------------------- constants
+constexpr int kAlgoSW = 0;
+constexpr int kAlgoTB = 1;
+constexpr int kOpAcquire = 0;
+constexpr int kOpPeek = 1;
+constexpr int kOpReset = 2;
+
+constexpr int64_t kRemUnknown = -1;   // TB permits > max
+constexpr int64_t kRemInvalid = -2;   // permits <= 0 / unknown limiter
+constexpr int64_t kRemError = -3;     // state-table region full
+
+// State table: a limiter's keys live in 2^k regions of kRegionSlots slots. One
+// workgroup owns a region for a whole batch, so a region needs no atomics in HBM.
+constexpr int kRegionSlots = 512;                 // slots per region (load <= ~0.5)
+constexpr int kRegionThreads = 256;               // workgroup of the region kernel
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// Partition tiles (upsweep / scatter / unpermute all share this tiling).
+constexpr int kTileThreads = 256;
+constexpr int kTileItems = 64;
+constexpr int kTile = kTileThreads * kTileItems;  // 16384 requests per tile
+constexpr int kMaxDigitBits = 12;                 // <= 4096 bins per pass
+
+// Compact record field limits.
+constexpr uint32_t kPermitBits = 22;
+constexpr uint32_t kPermitMask = (1u << kPermitBits) - 1;   // 0 = invalid marker
+constexpr int64_t kCompactMaxPermits = (int64_t)kPermitMask - 1;  // clamp is exact below this
+
+// ---------------------------------------------------------------- limiter table
+struct DevLimiter {          // 64 B, read-only during a batch
+    int32_t algo;
+    int32_t region_bits;     // k: the limiter has 2^k regions
+    uint32_t region_base;    // first global region id
+    uint32_t pad0;
+    int64_t max_permits;
+    int64_t window_ms;       // w
+    int64_t ttl_ms;          // SW: w (PEXPIRE on INCR); TB: 2w (Lua PEXPIRE)
+    double rate_per_ms;      // TB: refillRate / 1000.0 (TokenBucketRateLimiter.java:85)
+    double capacity;         // TB: (double)maxPermits (Lua tonumber(ARGV[1]))
+    uint64_t table;          // device address of this limiter's region array
+};
+
+// One 32-byte slot of a region (HBM and the LDS image).
+//   TB: a = tokens (f64 bits), b = last_refill ms (i64), c = bit0 "bucket exists"
+//   SW: a = start of the newest bucket b1 (i64)
+//       b = b1_count (u32) | b0_count (u32) << 32        (b0 = bucket at b1_start - w)
+//       c = b1_last_off (i32) | b0_last_off (i32) << 32  (last INCR time - bucket start)
+// A slot whose state is absent (TB c == 0, SW both counts 0) is free.
+struct Slot {
+    uint64_t tag;            // mix64(key_hash)
+    uint64_t a, b, c;
+};
+
+// ---------------------------------------------------------------- hashing
+// splitmix64 finaliser: a bijection on u64, so tags identify keys exactly.
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27; x *= 0x94d049bb133111ebULL;
+    x ^= x >> 31;
+    return x;
+}
+
+// owner shard = top s bits of h; region = next k bits.
+__host__ __device__ inline uint32_t region_local(uint64_t h, int shard_bits, int k) {
+    if (k == 0) return 0;
+    return (uint32_t)((h << shard_bits) >> (64 - k));
+}
+
+__host__ __device__ inline int64_t floor_div_ms(int64_t ns) {
+    int64_t q = ns / 1000000;
+    if ((ns % 1000000) != 0 && ns < 0) q -= 1;
+    return q;
+}
+
+// ---------------------------------------------------------------- records
+// Compact (16 B): {h, now_ms - base (u32), permits:22 | op:2 | limiter:8}.
+// Valid when every limiter has max_permits <= kCompactMaxPermits (so clamping the
+// permits field is decision-exact: SW est >= 0, TB early-rejects p > max) and the
+// batch's now_ms lies within +-2^31 ms of the first request's.
+struct RecC { uint64_t h; uint32_t now_rel; uint32_t pl; };
+// Wide (32 B): no limits beyond the engine's.
+struct RecW { uint64_t h; int64_t now_ms; int32_t permits; uint16_t limiter; uint8_t op;
+              uint8_t invalid; uint64_t pad; };
+
+struct Req {                 // decoded request
+    uint64_t h;
+    int64_t now_ms;
+    int32_t permits;         // >= 1 when valid (compact: clamped)
+    uint32_t limiter;
+    uint32_t op;
+    bool invalid;
+};
+
+struct CodecC {
+    using Rec = RecC;
+    __device__ static inline Rec enc(uint64_t h, int64_t now_ms, int64_t base, int32_t permits,
+                                     uint32_t op, uint32_t lim, bool invalid) {
+        Rec r;
+        r.h = h;
+        r.now_rel = (uint32_t)(now_ms - base);
+        uint32_t p = 0;
+        if (!invalid) {
+            if (op != (uint32_t)kOpAcquire) p = 1;
+            else p = (uint32_t)permits > kPermitMask ? kPermitMask : (uint32_t)permits;
+        }
+        r.pl = p | (op << kPermitBits) | (lim << 24);
+        return r;
+    }
+    __device__ static inline Req dec(const Rec& r, int64_t base) {
+        Req q;
+        q.h = r.h;
+        q.now_ms = base + (int64_t)r.now_rel;
+        q.permits = (int32_t)(r.pl & kPermitMask);
+        q.op = (r.pl >> kPermitBits) & 3u;
+        q.limiter = r.pl >> 24;
+        q.invalid = q.permits == 0;
+        return q;
+    }
+    __device__ static inline uint32_t limiter_of(const Rec& r) { return r.pl >> 24; }
+};
+
+struct CodecW {
+    using Rec = RecW;
+    __device__ static inline Rec enc(uint64_t h, int64_t now_ms, int64_t, int32_t permits,
+                                     uint32_t op, uint32_t lim, bool invalid) {
+        Rec r;
+        r.h = h; r.now_ms = now_ms; r.permits = permits; r.limiter = (uint16_t)lim;
+        r.op = (uint8_t)op; r.invalid = invalid ? 1 : 0; r.pad = 0;
+        return r;
+    }
+    __device__ static inline Req dec(const Rec& r, int64_t) {
+        Req q;
+        q.h = r.h; q.now_ms = r.now_ms; q.permits = r.permits; q.op = r.op;
+        q.limiter = r.limiter; q.invalid = r.invalid != 0;
+        return q;
+    }
+    __device__ static inline uint32_t limiter_of(const Rec& r) { return r.limiter; }
+};
+
+// ---------------------------------------------------------------- results
+// Packed 8-byte result in partition order: remaining << 1 | allowed.
+__device__ inline uint64_t pack_result(bool allowed, int64_t remaining) {
+    return ((uint64_t)remaining << 1) | (allowed ? 1u : 0u);
+}
+
+// Java (long) narrowing of a double (JLS 5.1.3) / Redis (long long) of a Lua number.
+__device__ inline int64_t d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+
+struct Outcome {
+    bool mutate;             // the request changes the key's state
+    bool allowed;
+    int64_t remaining;
+    double tokens;           // TB fp64 balance (NaN otherwise)
+    uint64_t a, b, c;        // new state when mutate
+};
+
+// ---------------------------------------------------------------- token bucket
+// TokenBucketRateLimiter.tryAcquire (:105-143) + Lua (:38-68). `last` is the ms
+// timestamp stored by HMSET; the bucket exists iff written and now <= last + 2w.
+__device__ inline Outcome tb_step(const DevLimiter& L, uint32_t op, int32_t permits,
+                                  int64_t now, uint64_t a, uint64_t b, uint64_t c) {
+    Outcome o;
+    o.mutate = false; o.allowed = false; o.remaining = 0; o.tokens = __builtin_nan("");
+    o.a = a; o.b = b; o.c = c;
+    const int64_t last = (int64_t)b;
+    const bool exists = (c & 1u) && !(now > last + L.ttl_ms);
+    const double capacity = L.capacity;
+    if (op == (uint32_t)kOpReset) {                  // DEL tb:key (:153-158)
+        o.mutate = true; o.a = 0; o.b = 0; o.c = 0;
+        return o;
+    }
+    if (op == (uint32_t)kOpAcquire && (int64_t)permits > L.max_permits) {  // :110-116
+        o.remaining = kRemUnknown;
+        return o;
+    }
+    const double nowd = (double)now;
+    double tokens = exists ? __longlong_as_double((long long)a) : capacity;
+    const double last_refill = exists ? (double)last : nowd;
+    const double elapsed = nowd - last_refill;               // Lua :56
+    const double tokens_to_add = elapsed * L.rate_per_ms;    // Lua :57
+    const double x = tokens + tokens_to_add;                 // Lua :58
+    tokens = x < capacity ? x : capacity;                    // math.min(capacity, x)
+    if (op == (uint32_t)kOpPeek) {
+        o.remaining = d2l(tokens);
+        o.tokens = tokens;
+        return o;
+    }
+    const double requested = (double)permits;
+    if (tokens >= requested) {                               // Lua :61-65
+        tokens = tokens - requested;
+        o.mutate = true; o.allowed = true;
+        o.a = (uint64_t)__double_as_longlong(tokens);
+        o.b = (uint64_t)now;
+        o.c = 1;
+    }
+    o.remaining = d2l(tokens);                               // {allowed, tokens} reply
+    o.tokens = tokens;
+    return o;
+}
+
+// ---------------------------------------------------------------- sliding window
+struct SW2 {                 // the two most recent buckets of a key
+    int64_t b1_start;
+    uint32_t b1_cnt, b0_cnt;
+    int32_t b1_off, b0_off;
+};
+
+__device__ inline SW2 sw_unpack(uint64_t a, uint64_t b, uint64_t c) {
+    SW2 s;
+    s.b1_start = (int64_t)a;
+    s.b1_cnt = (uint32_t)b; s.b0_cnt = (uint32_t)(b >> 32);
+    s.b1_off = (int32_t)(uint32_t)c; s.b0_off = (int32_t)(uint32_t)(c >> 32);
+    return s;
+}
+
+// RedisRateLimitStorage.get (:52-59) of bucket `start` at `now`: 0 if missing or
+// expired (PEXPIRE w on every INCR; expired iff now > lastIncr + w).
+__device__ inline int64_t sw_get(const SW2& s, int64_t start, int64_t now, int64_t w) {
+    if (s.b1_cnt != 0 && s.b1_start == start && !(now > s.b1_start + s.b1_off + w))
+        return s.b1_cnt;
+    const int64_t b0_start = s.b1_start - w;
+    if (s.b0_cnt != 0 && b0_start == start && !(now > b0_start + s.b0_off + w))
+        return s.b0_cnt;
+    return 0;
+}
+
+// getCurrentCount (SlidingWindowRateLimiter.java:158-180).
+__device__ inline int64_t sw_estimate(const SW2& s, int64_t now, int64_t w) {
+    const int64_t curr_start = (now / w) * w;                 // getWindowKey :186
+    const int64_t prev_start = ((now - w) / w) * w;
+    const int64_t curr = sw_get(s, curr_start, now, w);
+    const int64_t prev = sw_get(s, prev_start, now, w);
+    const double pct = (double)(now % w) / (double)w;         // :170
+    const double prev_weight = 1.0 - pct;                     // :171
+    const double t = (double)prev * prev_weight;              // :174, rounded
+    const double sum = t + (double)curr;                      //       rounded separately
+    return d2l(sum);
+}
+
+__device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t permits,
+                                  int64_t now, uint64_t a, uint64_t b, uint64_t c) {
+    Outcome o;
+    o.mutate = false; o.allowed = false; o.remaining = 0; o.tokens = __builtin_nan("");
+    o.a = a; o.b = b; o.c = c;
+    const int64_t w = L.window_ms;
+    SW2 s = sw_unpack(a, b, c);
+    const int64_t curr_start = (now / w) * w;
+    if (op == (uint32_t)kOpReset) {                  // reset (:139-153): DEL curr and prev
+        const int64_t prev_start = ((now - w) / w) * w;
+        if (s.b1_start == curr_start || s.b1_start == prev_start) s.b1_cnt = 0;
+        const int64_t b0_start = s.b1_start - w;
+        if (b0_start == curr_start || b0_start == prev_start) s.b0_cnt = 0;
+        o.mutate = true;
+        o.b = (uint64_t)s.b1_cnt | ((uint64_t)s.b0_cnt << 32);
+        return o;
+    }
+    const int64_t est = sw_estimate(s, now, w);
+    if (op == (uint32_t)kOpPeek || est + (int64_t)permits > L.max_permits) {  // :104
+        const int64_t r = L.max_permits - est;
+        o.remaining = r > 0 ? r : 0;
+        return o;
+    }
+    // incrementAndExpire(currentKey, w) (:114-116, RedisRateLimitStorage.java:38-49)
+    if (s.b1_start == curr_start) {
+        const bool alive = s.b1_cnt != 0 && !(now > s.b1_start + s.b1_off + w);
+        s.b1_cnt = alive ? s.b1_cnt + 1 : 1;
+    } else {                                         // a newer window (now is per-key monotone)
+        if (s.b1_start == curr_start - w) { s.b0_cnt = s.b1_cnt; s.b0_off = s.b1_off; }
+        else { s.b0_cnt = 0; s.b0_off = 0; }
+        s.b1_start = curr_start;
+        s.b1_cnt = 1;
+    }
+    s.b1_off = (int32_t)(now - curr_start);
+    o.mutate = true;
+    o.allowed = (int64_t)s.b1_cnt <= L.max_permits;  // :123
+    const int64_t est2 = sw_estimate(s, now, w);     // remaining after the request (A4)
+    const int64_t r = L.max_permits - est2;
+    o.remaining = r > 0 ? r : 0;
+    o.a = (uint64_t)s.b1_start;
+    o.b = (uint64_t)s.b1_cnt | ((uint64_t)s.b0_cnt << 32);
+    o.c = (uint64_t)(uint32_t)s.b1_off | ((uint64_t)(uint32_t)s.b0_off << 32);
+    return o;
+}
+
+// A slot is kept when the region is loaded iff some request at now >= batch_min could
+// still read it; everything else is dropped (the region is rebuilt in LDS).
+__device__ inline bool slot_live(const DevLimiter& L, const Slot& s, int64_t batch_min) {
+    if (L.algo == kAlgoTB) {
+        return (s.c & 1u) && !(batch_min > (int64_t)s.b + L.ttl_ms);
+    }
+    SW2 q = sw_unpack(s.a, s.b, s.c);
+    const int64_t w = L.window_ms;
+    const bool l1 = q.b1_cnt != 0 && !(batch_min > q.b1_start + q.b1_off + w);
+    const bool l0 = q.b0_cnt != 0 && !(batch_min > q.b1_start - w + q.b0_off + w);
+    return l1 || l0;
+}
+
+__device__ inline bool state_present(int algo, uint64_t b, uint64_t c) {
+    return algo == kAlgoTB ? (c & 1u) != 0 : b != 0;
+}
+
+}  // namespace rl

@@ -1,0 +1,645 @@
+// rl_engine.cpp — host runtime behind include/rl_engine.h.
+//
+// Owns, per GPU: the HBM state table (one region array per limiter), the
+// limiter table, the batch scratch and one HIP stream. A batch is a fixed chain
+// of kernel launches on that stream (see rl_kernels.hip); nothing in the chain
+// synchronises with the host, so the device entry point is fully asynchronous.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/rl_engine.h"
+#include "rl_launch.hpp"
+
+using namespace rl;
+
+namespace {
+
+constexpr int kStages = 6;
+const char* kStageNames[kStages] = {"partition0", "partition1", "region_offsets", "region",
+                                    "unpermute", "total"};
+
+struct HostLimiter {
+    rl_limiter_config cfg;
+    DevLimiter dev;
+    void* table = nullptr;
+    size_t table_bytes = 0;
+};
+
+inline int ceil_log2(uint64_t x) {
+    int b = 0;
+    while ((1ULL << b) < x) ++b;
+    return b;
+}
+
+}  // namespace
+
+struct rl_engine {
+    int device = 0;
+    rl_opts opts{};
+    int shard_bits = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;                          // one batch in flight per engine handle
+
+    std::vector<HostLimiter> lims;
+    uint32_t n_regions = 0;
+    DevLimiter* d_lims = nullptr;
+    uint8_t* d_region_lim = nullptr;
+    size_t region_lim_cap = 0;
+
+    // scratch (sized for opts.max_batch)
+    size_t cap_n = 0;
+    bool cap_wide = false;
+    void* rec0 = nullptr;
+    void* rec1 = nullptr;
+    uint32_t* pos0 = nullptr;
+    uint32_t* pos1 = nullptr;
+    uint64_t* res = nullptr;
+    double* tok = nullptr;
+    uint32_t* counts = nullptr;             // [bins][tiles]
+    size_t counts_cap = 0;
+    uint32_t* bin_total = nullptr;          // [4096]
+    uint32_t* bin_base = nullptr;           // [4096]
+    uint32_t* region_count = nullptr;       // [P padded]
+    uint32_t* region_start = nullptr;
+    uint32_t* row_tmp = nullptr;
+    uint32_t* row_base = nullptr;
+    size_t region_cap = 0;
+    BatchCtl* d_ctl = nullptr;
+    BatchCtl* h_ctl = nullptr;              // pinned copy of the last batch's ctl
+
+    // host-API staging (device copies of caller buffers)
+    size_t stage_cap = 0;
+    uint64_t* s_key = nullptr;
+    int32_t* s_permits = nullptr;
+    int64_t* s_now = nullptr;
+    uint16_t* s_lim = nullptr;
+    uint8_t* s_op = nullptr;
+    uint8_t* s_allowed = nullptr;
+    int64_t* s_remaining = nullptr;
+    double* s_tokens = nullptr;
+
+    // routing scratch
+    uint32_t* route_scratch = nullptr;
+    size_t route_cap = 0;
+    uint32_t* route_counts = nullptr;
+
+    hipEvent_t ev[kStages + 1] = {};
+    float stage_ms[kStages] = {};
+    bool timing = false;
+    bool last_wide = false;
+    bool pending_status = false;
+    int last_status = RL_OK;
+    uint64_t last_n = 0;
+};
+
+#define HIP_OK(x)                                                      \
+    do {                                                               \
+        hipError_t _e = (x);                                           \
+        if (_e != hipSuccess) {                                        \
+            std::fprintf(stderr, "rl_engine: %s failed: %s (%s:%d)\n", #x, \
+                         hipGetErrorString(_e), __FILE__, __LINE__);   \
+            return RL_E_DEVICE;                                        \
+        }                                                              \
+    } while (0)
+
+static void dfree(void*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+template <class T>
+static void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+static int dalloc(void** p, size_t bytes) {
+    if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) {
+        *p = nullptr;
+        return RL_E_NOMEM;
+    }
+    return RL_OK;
+}
+template <class T>
+static int dalloc(T** p, size_t count) {
+    return dalloc((void**)p, count * sizeof(T));
+}
+
+extern "C" int rl_abi_version(void) { return RL_ABI_VERSION; }
+
+extern "C" const char* rl_strerror(int s) {
+    switch (s) {
+        case RL_OK: return "ok";
+        case RL_E_INVALID_ARG: return "invalid argument";
+        case RL_E_INVALID_REQUEST: return "invalid request(s) in batch (permits <= 0 or unknown limiter)";
+        case RL_E_CAPACITY: return "state-table region full";
+        case RL_E_DEVICE: return "HIP device error";
+        case RL_E_NOMEM: return "out of memory";
+        case RL_E_TOO_LARGE: return "batch larger than max_batch";
+        case RL_E_LIMITERS: return "too many limiters";
+        default: return "unknown status";
+    }
+}
+
+extern "C" uint32_t rl_owner_of(uint64_t key_hash, uint16_t, uint32_t shard_count) {
+    if (shard_count <= 1) return 0;
+    const int s = ceil_log2(shard_count);
+    return (uint32_t)(mix64(key_hash) >> (64 - s));
+}
+
+extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
+    if (!out) return RL_E_INVALID_ARG;
+    *out = nullptr;
+    rl_opts o{};
+    if (opts) o = *opts;
+    if (o.max_batch == 0) o.max_batch = 1u << 22;
+    if (o.max_batch > 0xFFFFFFF0ULL) return RL_E_INVALID_ARG;   // u32 positions
+    if (o.default_capacity == 0) o.default_capacity = 1u << 20;
+    if (o.shard_count == 0) o.shard_count = 1;
+    if ((o.shard_count & (o.shard_count - 1)) != 0 || o.shard_count > 64) return RL_E_INVALID_ARG;
+    if (o.shard_index >= o.shard_count) return RL_E_INVALID_ARG;
+    rl_engine* e = new (std::nothrow) rl_engine();
+    if (!e) return RL_E_NOMEM;
+    e->opts = o;
+    e->shard_bits = ceil_log2(o.shard_count);
+    if (o.device >= 0) {
+        if (hipSetDevice(o.device) != hipSuccess) { delete e; return RL_E_DEVICE; }
+        e->device = o.device;
+    } else {
+        (void)hipGetDevice(&e->device);
+    }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return RL_E_DEVICE;
+    }
+    e->timing = (o.flags & RL_OPT_STAGE_TIMING) != 0;
+    for (int i = 0; i <= kStages; ++i) (void)hipEventCreate(&e->ev[i]);
+    int rc = dalloc(&e->d_ctl, 1);
+    if (rc == RL_OK && hipHostMalloc((void**)&e->h_ctl, sizeof(BatchCtl)) != hipSuccess) rc = RL_E_NOMEM;
+    if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
+    if (rc == RL_OK) rc = dalloc(&e->bin_total, 1u << kMaxDigitBits);
+    if (rc == RL_OK) rc = dalloc(&e->bin_base, 1u << kMaxDigitBits);
+    if (rc != RL_OK) { rl_destroy(e); return rc; }
+    std::memset(e->h_ctl, 0, sizeof(BatchCtl));
+    *out = e;
+    return RL_OK;
+}
+
+extern "C" void rl_destroy(rl_engine* e) {
+    if (!e) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto& l : e->lims) dfree(l.table);
+    dfree(e->d_lims); dfree(e->d_region_lim);
+    dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
+    dfree(e->counts); dfree(e->bin_total); dfree(e->bin_base);
+    dfree(e->region_count); dfree(e->region_start); dfree(e->row_tmp); dfree(e->row_base);
+    dfree(e->d_ctl);
+    dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
+    dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
+    dfree(e->route_scratch); dfree(e->route_counts);
+    if (e->h_ctl) (void)hipHostFree(e->h_ctl);
+    for (int i = 0; i <= kStages; ++i) if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+static int upload_limiters(rl_engine* e) {
+    std::vector<DevLimiter> dv;
+    for (auto& l : e->lims) dv.push_back(l.dev);
+    HIP_OK(hipMemcpy(e->d_lims, dv.data(), dv.size() * sizeof(DevLimiter), hipMemcpyHostToDevice));
+    std::vector<uint8_t> map(e->n_regions);
+    for (size_t li = 0; li < e->lims.size(); ++li) {
+        const auto& d = e->lims[li].dev;
+        std::fill(map.begin() + d.region_base, map.begin() + d.region_base + (1u << d.region_bits),
+                  (uint8_t)li);
+    }
+    if (e->region_lim_cap < map.size()) {
+        dfree(e->d_region_lim);
+        if (dalloc(&e->d_region_lim, map.size()) != RL_OK) return RL_E_NOMEM;
+        e->region_lim_cap = map.size();
+    }
+    HIP_OK(hipMemcpy(e->d_region_lim, map.data(), map.size(), hipMemcpyHostToDevice));
+    return RL_OK;
+}
+
+extern "C" int rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* c, uint16_t* id) {
+    if (!e || !c) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    // RateLimitConfig.validate() (RateLimitConfig.java:46-56)
+    if (c->max_permits <= 0 || c->window_ms <= 0 || !(c->refill_per_s >= 0.0)) return RL_E_INVALID_ARG;
+    if (c->algo == RL_ALGO_TOKEN_BUCKET && !(c->refill_per_s > 0.0)) return RL_E_INVALID_ARG;  // TB ctor :77-79
+    if (c->algo != RL_ALGO_TOKEN_BUCKET && c->algo != RL_ALGO_SLIDING_WINDOW) return RL_E_INVALID_ARG;
+    if (c->window_ms > RL_MAX_WINDOW_MS) return RL_E_INVALID_ARG;
+    if (c->algo == RL_ALGO_SLIDING_WINDOW && c->max_permits > RL_SW_MAX_PERMITS_LIMIT) return RL_E_INVALID_ARG;
+    if (c->algo == RL_ALGO_TOKEN_BUCKET && c->max_permits > RL_TB_MAX_PERMITS_LIMIT) return RL_E_INVALID_ARG;
+    if (e->lims.size() >= RL_MAX_LIMITERS) return RL_E_LIMITERS;
+    (void)hipSetDevice(e->device);
+    HostLimiter h;
+    h.cfg = *c;
+    uint64_t cap = c->capacity ? c->capacity : e->opts.default_capacity;
+    uint64_t per_shard = (cap + e->opts.shard_count - 1) / e->opts.shard_count;
+    uint64_t slots = std::max<uint64_t>(per_shard * 2, kRegionSlots);   // load <= 0.5
+    uint64_t regions = (slots + kRegionSlots - 1) / kRegionSlots;
+    int k = ceil_log2(regions);
+    if (k + e->shard_bits > 40) return RL_E_INVALID_ARG;
+    if ((uint64_t)e->n_regions + (1ULL << k) > (1ULL << 24)) return RL_E_LIMITERS;
+    DevLimiter& d = h.dev;
+    std::memset(&d, 0, sizeof(d));
+    d.algo = c->algo;
+    d.region_bits = k;
+    d.region_base = e->n_regions;
+    d.max_permits = c->max_permits;
+    d.window_ms = c->window_ms;
+    d.ttl_ms = c->algo == RL_ALGO_TOKEN_BUCKET ? c->window_ms * 2 : c->window_ms;
+    d.rate_per_ms = c->refill_per_s / 1000.0;        // TokenBucketRateLimiter.java:85
+    d.capacity = (double)c->max_permits;
+    h.table_bytes = (size_t)(1ULL << k) * kRegionSlots * sizeof(Slot);
+    if (dalloc(&h.table, h.table_bytes) != RL_OK) return RL_E_NOMEM;
+    if (hipMemset(h.table, 0, h.table_bytes) != hipSuccess) { dfree(h.table); return RL_E_DEVICE; }
+    d.table = (uint64_t)(uintptr_t)h.table;
+    e->lims.push_back(h);
+    e->n_regions += 1u << k;
+    int rc = upload_limiters(e);
+    if (rc != RL_OK) return rc;
+    if (id) *id = (uint16_t)(e->lims.size() - 1);
+    return RL_OK;
+}
+
+extern "C" int rl_add_limiter(rl_engine* e, int algo, int64_t max_permits, int64_t window_ms,
+                              double refill_per_s, uint16_t* id) {
+    rl_limiter_config c{};
+    c.algo = algo;
+    c.max_permits = max_permits;
+    c.window_ms = window_ms;
+    c.refill_per_s = refill_per_s;
+    c.capacity = 0;
+    return rl_add_limiter_ex(e, &c, id);
+}
+
+static int ensure_scratch(rl_engine* e, size_t n, bool wide, uint32_t bins, uint32_t n_tiles) {
+    if (n > e->cap_n || (wide && !e->cap_wide)) {
+        size_t cap = std::max<size_t>(n, std::min<size_t>(e->opts.max_batch, std::max<size_t>(n, 1u << 20)));
+        const size_t rb = wide ? sizeof(RecW) : sizeof(RecC);
+        dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
+        int rc = dalloc(&e->rec0, cap * rb);
+        if (rc == RL_OK) rc = dalloc(&e->rec1, cap * rb);
+        if (rc == RL_OK) rc = dalloc(&e->pos0, cap);
+        if (rc == RL_OK) rc = dalloc(&e->pos1, cap);
+        if (rc == RL_OK) rc = dalloc(&e->res, cap);
+        if (rc == RL_OK) rc = dalloc(&e->tok, cap);
+        if (rc != RL_OK) { e->cap_n = 0; return rc; }
+        e->cap_n = cap;
+        e->cap_wide = wide;
+    }
+    const size_t need_counts = (size_t)bins * n_tiles;
+    if (need_counts > e->counts_cap) {
+        dfree(e->counts);
+        size_t c = std::max(need_counts, (size_t)(1u << kMaxDigitBits) *
+                                              ((std::max<size_t>(n, e->opts.max_batch) + kTile - 1) / kTile));
+        if (dalloc(&e->counts, c) != RL_OK) return RL_E_NOMEM;
+        e->counts_cap = c;
+    }
+    return RL_OK;
+}
+
+static int ensure_regions(rl_engine* e, size_t padded) {
+    if (padded <= e->region_cap) return RL_OK;
+    dfree(e->region_count); dfree(e->region_start); dfree(e->row_tmp); dfree(e->row_base);
+    int rc = dalloc(&e->region_count, padded);
+    if (rc == RL_OK) rc = dalloc(&e->region_start, padded);
+    if (rc == RL_OK) rc = dalloc(&e->row_tmp, padded / 4096 + 1);
+    if (rc == RL_OK) rc = dalloc(&e->row_base, padded / 4096 + 1);
+    if (rc != RL_OK) return rc;
+    e->region_cap = padded;
+    return RL_OK;
+}
+
+static inline void mark(rl_engine* e, int i) {
+    if (e->timing) (void)hipEventRecord(e->ev[i], e->stream);
+}
+
+// The pipeline on device buffers, enqueued on e->stream. Returns an immediate status
+// (argument/launch errors); the data-dependent status is read back by rl_last_status.
+static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const int32_t* permits,
+                            const int64_t* now_ns, const uint16_t* limiter, const uint8_t* op,
+                            uint8_t* allowed, int64_t* remaining, double* tokens_after) {
+    if (n > e->opts.max_batch) return RL_E_TOO_LARGE;
+    e->last_n = n;
+    e->pending_status = false;
+    e->last_status = RL_OK;
+    if (n == 0) return RL_OK;
+    if (!key || !permits || !now_ns || !allowed || !remaining) return RL_E_INVALID_ARG;
+    hipStream_t s = e->stream;
+    if (e->lims.empty()) {
+        HIP_OK(launch_fill_invalid(allowed, remaining, tokens_after, (uint32_t)n, s));
+        e->last_status = RL_E_INVALID_REQUEST;
+        return RL_OK;
+    }
+    bool wide = false;
+    for (auto& l : e->lims) wide |= l.cfg.max_permits > kCompactMaxPermits;
+    const uint32_t nt = (uint32_t)((n + kTile - 1) / kTile);
+    const int bitsP = std::max(1, ceil_log2(e->n_regions));
+    const int passes = bitsP <= kMaxDigitBits ? 1 : 2;
+    if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
+    const int d0 = passes == 1 ? bitsP : bitsP - bitsP / 2;
+    const int d1 = bitsP - d0;
+    int rc = ensure_scratch(e, n, wide, 1u << std::max(d0, d1), nt);
+    if (rc != RL_OK) return rc;
+    const uint32_t cols = 4096;
+    const size_t padded = ((size_t)e->n_regions + cols - 1) / cols * cols;
+    if (passes == 2) {
+        rc = ensure_regions(e, padded);
+        if (rc != RL_OK) return rc;
+    }
+    e->last_wide = wide;
+
+    mark(e, 0);
+    PartArgs pa{};
+    pa.key = key; pa.permits = permits; pa.now_ns = now_ns; pa.limiter = limiter; pa.op = op;
+    pa.n = (uint32_t)n; pa.n_tiles = nt; pa.n_lim = (uint32_t)e->lims.size();
+    pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = e->d_ctl;
+    pa.counts = e->counts; pa.bin_base = e->bin_base;
+    // ---- pass 0 (low digit) from the caller's arrays
+    pa.digit_shift = 0; pa.digit_bits = d0;
+    pa.region_count = nullptr;
+    if (passes == 2) {
+        HIP_OK(hipMemsetAsync(e->region_count, 0, padded * sizeof(uint32_t), s));
+        pa.region_count = e->region_count;
+    }
+    pa.rec_out = e->rec0; pa.pos_out = e->pos0;
+    HIP_OK(launch_upsweep(pa, true, wide, s));
+    HIP_OK(launch_scan_rows(e->counts, e->counts, 1u << d0, nt, e->bin_total, s));
+    HIP_OK(launch_scan_small(e->bin_total, e->bin_base, 1u << d0, s));
+    HIP_OK(launch_scatter(pa, true, wide, s));
+    mark(e, 1);
+    const void* rec_final = e->rec0;
+    const uint32_t* rstart = e->bin_base;
+    const uint32_t* rcount = e->bin_total;
+    if (passes == 2) {
+        // ---- pass 1 (high digit) over the records; stable, so the final order is
+        // region-major and arrival-ordered inside each region.
+        pa.region_count = nullptr;
+        pa.digit_shift = d0; pa.digit_bits = d1;
+        pa.rec_in = e->rec0; pa.rec_out = e->rec1; pa.pos_out = e->pos1;
+        HIP_OK(launch_upsweep(pa, false, wide, s));
+        HIP_OK(launch_scan_rows(e->counts, e->counts, 1u << d1, nt, e->bin_total, s));
+        HIP_OK(launch_scan_small(e->bin_total, e->bin_base, 1u << d1, s));
+        HIP_OK(launch_scatter(pa, false, wide, s));
+        rec_final = e->rec1;
+    }
+    mark(e, 2);
+    if (passes == 2) {
+        const uint32_t rows = (uint32_t)(padded / cols);
+        HIP_OK(launch_scan_rows(e->region_count, e->region_start, rows, cols, e->row_tmp, s));
+        HIP_OK(launch_scan_small(e->row_tmp, e->row_base, rows, s));
+        HIP_OK(launch_add_rows(e->row_base, e->region_start, rows, cols, s));
+        rstart = e->region_start;
+        rcount = e->region_count;
+    }
+    mark(e, 3);
+    RegionArgs ra{};
+    ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.region_lim = e->d_region_lim;
+    ra.lims = e->d_lims; ra.res = e->res; ra.tok = tokens_after ? e->tok : nullptr;
+    ra.ctl = e->d_ctl; ra.n_regions = e->n_regions;
+    HIP_OK(launch_region(ra, wide, s));
+    mark(e, 4);
+    UnpermArgs ua{};
+    ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
+    ua.tok = tokens_after ? e->tok : nullptr;
+    ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
+    ua.n = (uint32_t)n; ua.n_tiles = nt;
+    HIP_OK(launch_unpermute(ua, s));
+    mark(e, 5);
+    HIP_OK(hipMemcpyAsync(e->h_ctl, e->d_ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, s));
+    e->pending_status = true;
+    return RL_OK;
+}
+
+static int collect_status(rl_engine* e) {
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (!e->pending_status) return e->last_status;
+    e->pending_status = false;
+    if (e->timing) {
+        float ms;
+        const int pairs[kStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {0, 5}};
+        for (int i = 0; i < kStages; ++i) {
+            e->stage_ms[i] = hipEventElapsedTime(&ms, e->ev[pairs[i][0]], e->ev[pairs[i][1]]) == hipSuccess ? ms : -1.f;
+        }
+    }
+    const BatchCtl& c = *e->h_ctl;
+    int st = RL_OK;
+    if (c.invalid) st = RL_E_INVALID_REQUEST;
+    if (c.cap_err) st = RL_E_CAPACITY;
+    if (c.span_overflow) st = RL_E_INVALID_ARG;
+    e->last_status = st;
+    return st;
+}
+
+extern "C" int rl_execute_batch_device(rl_engine* e, size_t n, const uint64_t* key,
+                                       const int32_t* permits, const int64_t* now_ns,
+                                       const uint16_t* limiter, const uint8_t* op,
+                                       uint8_t* allowed, int64_t* remaining, double* tokens_after,
+                                       void* stream) {
+    if (!e) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    hipStream_t user = (hipStream_t)stream;
+    if (user && user != e->stream) {
+        // order the engine stream after the caller's work, and the caller's after ours
+        hipEvent_t ev;
+        HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_OK(hipEventRecord(ev, user));
+        HIP_OK(hipStreamWaitEvent(e->stream, ev, 0));
+        int rc = run_batch_device(e, n, key, permits, now_ns, limiter, op, allowed, remaining,
+                                  tokens_after);
+        HIP_OK(hipEventRecord(ev, e->stream));
+        HIP_OK(hipStreamWaitEvent(user, ev, 0));
+        (void)hipEventDestroy(ev);
+        return rc;
+    }
+    return run_batch_device(e, n, key, permits, now_ns, limiter, op, allowed, remaining,
+                            tokens_after);
+}
+
+extern "C" int rl_last_status(rl_engine* e) {
+    if (!e) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    return collect_status(e);
+}
+
+static int ensure_staging(rl_engine* e, size_t n) {
+    if (n <= e->stage_cap) return RL_OK;
+    dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
+    dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
+    int rc = dalloc(&e->s_key, n);
+    if (rc == RL_OK) rc = dalloc(&e->s_permits, n);
+    if (rc == RL_OK) rc = dalloc(&e->s_now, n);
+    if (rc == RL_OK) rc = dalloc(&e->s_lim, n);
+    if (rc == RL_OK) rc = dalloc(&e->s_op, n);
+    if (rc == RL_OK) rc = dalloc(&e->s_allowed, n);
+    if (rc == RL_OK) rc = dalloc(&e->s_remaining, n);
+    if (rc == RL_OK) rc = dalloc(&e->s_tokens, n);
+    if (rc != RL_OK) { e->stage_cap = 0; return rc; }
+    e->stage_cap = n;
+    return RL_OK;
+}
+
+extern "C" int rl_execute_batch(rl_engine* e, size_t n, const uint64_t* key,
+                                const int32_t* permits, const int64_t* now_ns,
+                                const uint16_t* limiter, const uint8_t* op, uint8_t* allowed,
+                                int64_t* remaining, double* tokens_after) {
+    if (!e) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (n > e->opts.max_batch) return RL_E_TOO_LARGE;
+    if (n == 0) return RL_OK;
+    if (!key || !permits || !now_ns || !allowed || !remaining) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    int rc = ensure_staging(e, n);
+    if (rc != RL_OK) return rc;
+    hipStream_t s = e->stream;
+    HIP_OK(hipMemcpyAsync(e->s_key, key, n * 8, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->s_permits, permits, n * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(e->s_now, now_ns, n * 8, hipMemcpyHostToDevice, s));
+    if (limiter) HIP_OK(hipMemcpyAsync(e->s_lim, limiter, n * 2, hipMemcpyHostToDevice, s));
+    if (op) HIP_OK(hipMemcpyAsync(e->s_op, op, n, hipMemcpyHostToDevice, s));
+    rc = run_batch_device(e, n, e->s_key, e->s_permits, e->s_now, limiter ? e->s_lim : nullptr,
+                          op ? e->s_op : nullptr, e->s_allowed, e->s_remaining,
+                          tokens_after ? e->s_tokens : nullptr);
+    if (rc != RL_OK) { (void)hipStreamSynchronize(s); return rc; }
+    HIP_OK(hipMemcpyAsync(allowed, e->s_allowed, n, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(remaining, e->s_remaining, n * 8, hipMemcpyDeviceToHost, s));
+    if (tokens_after) HIP_OK(hipMemcpyAsync(tokens_after, e->s_tokens, n * 8, hipMemcpyDeviceToHost, s));
+    return collect_status(e);
+}
+
+extern "C" int rl_try_acquire_batch(rl_engine* e, size_t n, const uint64_t* key_hash,
+                                    const int32_t* permits, const int64_t* now_ns,
+                                    const uint16_t* limiter, uint8_t* allowed, int64_t* remaining,
+                                    double* tokens_after) {
+    return rl_execute_batch(e, n, key_hash, permits, now_ns, limiter, nullptr, allowed, remaining,
+                            tokens_after);
+}
+
+static int admin_op(rl_engine* e, uint16_t limiter, size_t n, const uint64_t* key,
+                    const int64_t* now_ns, uint8_t opcode, int64_t* out) {
+    if (!e || (n && (!key || !now_ns))) return RL_E_INVALID_ARG;
+    if (limiter >= e->lims.size()) return RL_E_INVALID_ARG;
+    if (n == 0) return RL_OK;
+    std::vector<int32_t> p(n, 1);
+    std::vector<uint16_t> l(n, limiter);
+    std::vector<uint8_t> o(n, opcode), a(n);
+    std::vector<int64_t> r(n);
+    int rc = rl_execute_batch(e, n, key, p.data(), now_ns, l.data(), o.data(), a.data(), r.data(),
+                              nullptr);
+    if (out) std::memcpy(out, r.data(), n * sizeof(int64_t));
+    return rc;
+}
+
+extern "C" int rl_available(rl_engine* e, uint16_t limiter, size_t n, const uint64_t* key_hash,
+                            const int64_t* now_ns, int64_t* available) {
+    if (!available && n) return RL_E_INVALID_ARG;
+    return admin_op(e, limiter, n, key_hash, now_ns, RL_OP_PEEK, available);
+}
+
+extern "C" int rl_reset(rl_engine* e, uint16_t limiter, size_t n, const uint64_t* key_hash,
+                        const int64_t* now_ns) {
+    return admin_op(e, limiter, n, key_hash, now_ns, RL_OP_RESET, nullptr);
+}
+
+extern "C" int rl_batch_stats_get(rl_engine* e, rl_batch_stats* out) {
+    if (!e || !out) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    collect_status(e);
+    const BatchCtl& c = *e->h_ctl;
+    out->n = e->last_n;
+    out->allowed = c.allowed;
+    out->distinct_keys = c.distinct;
+    out->invalid = c.invalid;
+    out->capacity_errors = c.cap_err;
+    out->regions_touched = c.regions;
+    out->table_bytes = c.regions * (uint64_t)kRegionSlots * sizeof(Slot) * 2;
+    return RL_OK;
+}
+
+extern "C" int rl_stage_times(rl_engine* e, const char** names, float* ms, int cap) {
+    if (!e) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    collect_status(e);
+    int k = std::min(cap, kStages);
+    for (int i = 0; i < k; ++i) {
+        if (names) names[i] = kStageNames[i];
+        if (ms) ms[i] = e->timing ? e->stage_ms[i] : -1.f;
+    }
+    return k;
+}
+
+extern "C" int rl_sync(rl_engine* e) {
+    if (!e) return RL_E_INVALID_ARG;
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return RL_OK;
+}
+
+extern "C" int rl_route_partition(rl_engine* e, size_t n, const uint64_t* key_hash,
+                                  const uint16_t*, uint32_t shard_count, uint32_t* perm,
+                                  uint64_t* counts_host, void* stream) {
+    if (!e || !key_hash || !perm || !counts_host) return RL_E_INVALID_ARG;
+    if (shard_count == 0 || shard_count > 64 || (shard_count & (shard_count - 1))) return RL_E_INVALID_ARG;
+    if (n > 0xFFFFFFF0ULL) return RL_E_TOO_LARGE;
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    const size_t nt = (n + kTile - 1) / kTile;
+    const size_t need = (size_t)shard_count * nt + 64;
+    if (need > e->route_cap) {
+        dfree(e->route_scratch);
+        if (dalloc(&e->route_scratch, need) != RL_OK) return RL_E_NOMEM;
+        e->route_cap = need;
+    }
+    if (!e->route_counts && dalloc(&e->route_counts, 64) != RL_OK) return RL_E_NOMEM;
+    if (n == 0) {
+        for (uint32_t i = 0; i < shard_count; ++i) counts_host[i] = 0;
+        return RL_OK;
+    }
+    HIP_OK(launch_owner_partition(key_hash, (uint32_t)n, shard_count, perm, e->route_counts,
+                                  e->route_scratch, s));
+    uint32_t c[64];
+    HIP_OK(hipMemcpyAsync(c, e->route_counts, shard_count * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    for (uint32_t i = 0; i < shard_count; ++i) counts_host[i] = c[i];
+    return RL_OK;
+}
+
+extern "C" int rl_synth_trace_device(rl_engine* e, const rl_trace_spec* sp, size_t n,
+                                     uint64_t* key_hash, int32_t* permits, int64_t* now_ns,
+                                     uint16_t* limiter, void* stream) {
+    if (!e || !sp || !key_hash || !permits || !now_ns) return RL_E_INVALID_ARG;
+    if (sp->n_keys == 0 || sp->permits_max <= 0 || sp->n_total == 0) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    SynthArgs a{};
+    a.seed = sp->seed; a.n_keys = sp->n_keys; a.dist = sp->dist; a.permits_max = sp->permits_max;
+    a.t0_ns = sp->t0_ns; a.span_ns = sp->span_ns; a.index_base = sp->index_base;
+    a.n_total = sp->n_total; a.n_limiters = sp->n_limiters ? sp->n_limiters : 1;
+    a.key = key_hash; a.permits = permits; a.now_ns = now_ns; a.limiter = limiter; a.n = n;
+    if (sp->dist == RL_DIST_ZIPF) {
+        const double s = sp->zipf_s;
+        if (!(s > 0.0) || s == 1.0) return RL_E_INVALID_ARG;
+        auto h1 = [](double x) { return std::fabs(x) > 1e-8 ? std::log1p(x) / x : 1.0 - x * (0.5 - x / 3.0); };
+        auto h2 = [](double x) { return std::fabs(x) > 1e-8 ? std::expm1(x) / x : 1.0 + x * 0.5 * (1.0 + x / 3.0); };
+        auto H = [&](double x) { double lx = std::log(x); return h2((1.0 - s) * lx) * lx; };
+        auto hh = [&](double x) { return std::exp(-s * std::log(x)); };
+        auto Hinv = [&](double x) { double t = x * (1.0 - s); if (t < -1.0) t = -1.0; return std::exp(h1(t) * x); };
+        a.zs = s;
+        a.hx1 = H(1.5) - 1.0;
+        a.hn = H((double)sp->n_keys + 0.5);
+        a.sconst = 2.0 - Hinv(H(2.5) - hh(2.0));
+    }
+    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_synth(a, st));
+    return RL_OK;
+}

@@ -1,0 +1,645 @@
+// rl_kernels.hip — the batched rate-limit decision pipeline for gfx950 (MI355X).
+//
+// One batch = requests in arrival order. The pipeline groups every request with
+// the other requests of its (limiter, key) WITHOUT a full sort:
+//
+//   1. k_upsweep  : per 16K-request tile, histogram of the partition digit of each
+//                   request's state-table REGION (region = top bits of mix64(key)).
+//   2. k_scan_rows/k_scan_small : exclusive scan of the [bin][tile] histogram.
+//   3. k_scatter  : stable partition (wave ballot-match ranking) of the requests
+//                   into region order, packed into 16-byte records.
+//   (2-3 repeat once more when a limiter set has > 4096 regions.)
+//   4. k_region   : one workgroup per region. Loads the region's 512 state slots
+//                   (16 KB) into LDS once, streams the region's records in arrival
+//                   order 256 at a time, applies the reference semantics per key in
+//                   order (deny never mutates, so a group needs 1 + (#state changes of
+//                   its busiest key) rounds), writes the region back once.
+//   5. k_unpermute: results back to the caller's order (allowed u8, remaining i64).
+//
+// Tiles are mapped XCD-aware (consecutive tiles on one XCD) so the per-tile
+// histogram columns, the record runs of one bin and the result gathers of
+// neighbouring tiles combine in that XCD's L2 instead of going to HBM as partial lines.
+#include "rl_launch.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rl {
+
+// ------------------------------------------------------------------ helpers
+__device__ inline uint32_t xcd_remap(uint32_t b, uint32_t n) {
+    // bijective: blocks b, b+8, ... (one XCD under round-robin dispatch) get
+    // consecutive tile ids.
+    const uint32_t q = n / 8, r = n % 8, x = b % 8;
+    const uint32_t base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    return base + b / 8;
+}
+
+__device__ inline uint32_t popc_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Lanes of this wave whose `v` (low nbits) equals mine, among `active` lanes.
+__device__ inline uint64_t wave_match(uint32_t v, int nbits, bool active) {
+    uint64_t m = __ballot(active);
+    for (int b = 0; b < nbits; ++b) {
+        const bool bit = (v >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+__device__ inline uint64_t ord_key(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ULL; }
+
+template <int NT>
+__device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_tmp /*[NT/64]*/,
+                                                uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) s_tmp[wid] = x;
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+    for (int w = 0; w < NT / 64; ++w) {
+        const uint32_t s = s_tmp[w];
+        if ((uint32_t)w < wid) wpre += s;
+        tot += s;
+    }
+    __syncthreads();
+    if (total) *total = tot;
+    return wpre + x - v;
+}
+
+struct LimLds {
+    uint32_t base[256];
+    uint8_t bits[256];
+};
+
+__device__ inline void load_lim_lds(LimLds& L, const PartArgs& a) {
+    for (uint32_t l = threadIdx.x; l < a.n_lim; l += blockDim.x) {
+        L.base[l] = a.lims[l].region_base;
+        L.bits[l] = (uint8_t)a.lims[l].region_bits;
+    }
+}
+
+// Global region id of element i (pass 0: raw arrays; later passes: records).
+template <class Codec, bool RAW>
+__device__ inline uint32_t region_of(const PartArgs& a, uint32_t i, const LimLds& L) {
+    uint64_t h;
+    uint32_t lim;
+    if constexpr (RAW) {
+        h = mix64(a.key[i]);
+        lim = a.limiter ? a.limiter[i] : 0u;
+        if (lim >= a.n_lim) lim = 0;  // invalid: routed to limiter 0's region, rejected there
+    } else {
+        const typename Codec::Rec* r = (const typename Codec::Rec*)a.rec_in + i;
+        h = r->h;
+        lim = Codec::limiter_of(*r);
+    }
+    return L.base[lim] + region_local(h, a.shard_bits, L.bits[lim]);
+}
+
+// ------------------------------------------------------------------ 1. upsweep
+template <class Codec, bool RAW>
+__global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
+    __shared__ uint32_t hist[1u << kMaxDigitBits];
+    __shared__ LimLds L;
+    const uint32_t t = threadIdx.x;
+    const uint32_t bins = 1u << a.digit_bits;
+    for (uint32_t b = t; b < bins; b += kTileThreads) hist[b] = 0;
+    load_lim_lds(L, a);
+    if constexpr (RAW) {
+        if (blockIdx.x == 0 && t == 0) {
+            BatchCtl* c = a.ctl;
+            c->base_ms = floor_div_ms(a.now_ns[0]) - (1LL << 31);
+            c->min_now_key = ~0ULL;
+            c->max_now_key = 0;
+            c->span_overflow = 0;
+            c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = 0;
+        }
+    }
+    __syncthreads();
+    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t mask = bins - 1;
+    for (int r = 0; r < kTileItems; ++r) {
+        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        if (i < a.n) {
+            const uint32_t g = region_of<Codec, RAW>(a, i, L);
+            atomicAdd(&hist[(g >> a.digit_shift) & mask], 1u);
+            if (a.region_count) atomicAdd(&a.region_count[g], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = t; b < bins; b += kTileThreads)
+        a.counts[(size_t)b * a.n_tiles + tile] = hist[b];
+}
+
+// ------------------------------------------------------------------ 2. scans
+// Exclusive scan of each row of a [rows][cols] matrix (one block per row).
+__global__ __launch_bounds__(256) void k_scan_rows(const uint32_t* in, uint32_t* out,
+                                                   uint32_t cols, uint32_t* totals) {
+    __shared__ uint32_t tmp[4];
+    const size_t row = blockIdx.x;
+    const uint32_t* src = in + row * cols;
+    uint32_t* dst = out + row * cols;
+    const uint32_t chunk = (cols + 255) / 256;
+    const uint32_t beg = min(threadIdx.x * chunk, cols);
+    const uint32_t end = min(beg + chunk, cols);
+    uint32_t sum = 0;
+    for (uint32_t k = beg; k < end; ++k) sum += src[k];
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<256>(sum, tmp, &tot);
+    for (uint32_t k = beg; k < end; ++k) {
+        const uint32_t v = src[k];
+        dst[k] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) totals[row] = tot;
+}
+
+// Single-block exclusive scan of a short array (<= a few million entries).
+__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* in, uint32_t* out,
+                                                     uint32_t len) {
+    __shared__ uint32_t tmp[16];
+    const uint32_t chunk = (len + 1023) / 1024;
+    const uint32_t beg = min(threadIdx.x * chunk, len);
+    const uint32_t end = min(beg + chunk, len);
+    uint32_t sum = 0;
+    for (uint32_t k = beg; k < end; ++k) sum += in[k];
+    uint32_t run = block_exclusive_scan<1024>(sum, tmp, nullptr);
+    for (uint32_t k = beg; k < end; ++k) {
+        const uint32_t v = in[k];
+        out[k] = run;
+        run += v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_add_rows(const uint32_t* row_base, uint32_t* data,
+                                                  uint32_t cols) {
+    const size_t row = blockIdx.x;
+    const uint32_t b = row_base[row];
+    for (uint32_t k = threadIdx.x; k < cols; k += 256) data[row * cols + k] += b;
+}
+
+// ------------------------------------------------------------------ 3. scatter
+// Stable: a tile's elements are ranked in (round, wave, lane) order, which is the
+// arrival order; tiles are ordered by the exclusive [bin][tile] scan.
+template <class Codec, bool RAW>
+__global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
+    using Rec = typename Codec::Rec;
+    __shared__ uint32_t cur[1u << kMaxDigitBits];                    // next slot per bin
+    __shared__ uint8_t cntw[kTileThreads / 64][1u << kMaxDigitBits]; // this round, per wave
+    __shared__ LimLds L;
+    __shared__ uint64_t s_mm[2][kTileThreads / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t bins = 1u << a.digit_bits, mask = bins - 1;
+    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+    for (uint32_t b = t; b < bins; b += kTileThreads) {
+        cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
+#pragma unroll
+        for (int w = 0; w < kTileThreads / 64; ++w) cntw[w][b] = 0;
+    }
+    load_lim_lds(L, a);
+    int64_t base = 0;
+    if constexpr (RAW) base = a.ctl->base_ms;
+    __syncthreads();
+    uint64_t mn = ~0ULL, mx = 0;
+    bool overflow = false;
+    for (int r = 0; r < kTileItems; ++r) {
+        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        const bool active = i < a.n;
+        Rec rec{};
+        uint32_t d = 0;
+        if (active) {
+            if constexpr (RAW) {
+                const uint64_t key = a.key[i];
+                uint32_t lim = a.limiter ? a.limiter[i] : 0u;
+                const int32_t p = a.permits[i];
+                const int64_t now_ms = floor_div_ms(a.now_ns[i]);
+                uint32_t op = a.op ? a.op[i] : 0u;
+                const bool lim_ok = lim < a.n_lim;
+                if (!lim_ok) lim = 0;
+                const bool invalid = !lim_ok || op > 2u || (op == 0u && p <= 0);
+                if (op > 2u) op = 0;
+                const uint64_t h = mix64(key);
+                rec = Codec::enc(h, now_ms, base, p, op, lim, invalid);
+                const int64_t rel = now_ms - base;
+                overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
+                const uint64_t k = ord_key(now_ms);
+                mn = k < mn ? k : mn;
+                mx = k > mx ? k : mx;
+                d = ((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.digit_shift) & mask;
+            } else {
+                rec = ((const Rec*)a.rec_in)[i];
+                const uint32_t lim = Codec::limiter_of(rec);
+                d = ((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.digit_shift) & mask;
+            }
+        }
+        const uint64_t m = wave_match(d, a.digit_bits, active);
+        const uint32_t lr = popc_below(m);
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        const bool leader = active && lr == 0;
+        if (leader) cntw[wid][d] = (uint8_t)cnt;
+        __syncthreads();
+        uint32_t pos = 0;
+        if (active) {
+            pos = cur[d] + lr;
+            for (uint32_t w = 0; w < wid; ++w) pos += cntw[w][d];
+        }
+        __syncthreads();
+        if (leader) {
+            atomicAdd(&cur[d], cnt);
+            cntw[wid][d] = 0;
+        }
+        if (active) {
+            ((Rec*)a.rec_out)[pos] = rec;
+            a.pos_out[i] = pos;
+        }
+    }
+    if constexpr (RAW) {
+        // min / max now over the tile -> one atomic each
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a1 = __shfl_xor(mn, o, 64), b1 = __shfl_xor(mx, o, 64);
+            mn = a1 < mn ? a1 : mn;
+            mx = b1 > mx ? b1 : mx;
+        }
+        if (lane == 0) { s_mm[0][wid] = mn; s_mm[1][wid] = mx; }
+        const bool any_over = __syncthreads_or(overflow);
+        if (t == 0) {
+            for (int w = 1; w < kTileThreads / 64; ++w) {
+                mn = s_mm[0][w] < mn ? s_mm[0][w] : mn;
+                mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
+            }
+            atomicMin((unsigned long long*)&a.ctl->min_now_key, (unsigned long long)mn);
+            atomicMax((unsigned long long*)&a.ctl->max_now_key, (unsigned long long)mx);
+            if (any_over) atomicOr(&a.ctl->span_overflow, 1u);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 4. region
+template <class Codec>
+__global__ __launch_bounds__(kRegionThreads) void k_region(RegionArgs a) {
+    using Rec = typename Codec::Rec;
+    constexpr uint32_t R = kRegionSlots;
+    __shared__ uint64_t s_tag[R], s_a[R], s_b[R], s_c[R];
+    __shared__ uint32_t s_occ[R];   // bit0 occupied, bit1 touched by this batch
+    __shared__ uint32_t s_fm[R];    // first mutating lane of the current round
+    __shared__ uint32_t s_stat[4];
+
+    const uint32_t g = blockIdx.x;
+    const uint32_t cnt = a.rcount[g];
+    if (cnt == 0) return;
+    const uint32_t start = a.rstart[g];
+    const uint32_t t = threadIdx.x;
+    const DevLimiter L = a.lims[a.region_lim[g]];
+    const bool tb = L.algo == kAlgoTB;
+    const bool span_bad = a.ctl->span_overflow != 0;
+    const int64_t base = a.ctl->base_ms;
+    const int64_t batch_min = (int64_t)(a.ctl->min_now_key ^ 0x8000000000000000ULL);
+    Slot* tab = (Slot*)L.table + (size_t)(g - L.region_base) * R;
+
+    for (uint32_t s = t; s < R; s += kRegionThreads) { s_occ[s] = 0; s_fm[s] = kNone; }
+    if (t < 4) s_stat[t] = 0;
+    __syncthreads();
+
+    if (span_bad) {
+        // compact records cannot represent this batch's time span: reject it whole,
+        // before any state is touched (the host reports RL_E_INVALID_ARG).
+        for (uint32_t j = start + t; j < start + cnt; j += kRegionThreads) {
+            a.res[j] = pack_result(false, kRemInvalid);
+            if (a.tok) a.tok[j] = __builtin_nan("");
+        }
+        return;
+    }
+
+    // Load the region, dropping entries no request of this batch can see, and
+    // rebuild the open-addressing table in LDS (no tombstones ever reach HBM).
+    for (uint32_t s = t; s < R; s += kRegionThreads) {
+        const Slot v = tab[s];
+        if (slot_live(L, v, batch_min)) {
+            uint32_t p = (uint32_t)v.tag & (R - 1);
+            while (atomicCAS(&s_occ[p], 0u, 1u) != 0u) p = (p + 1) & (R - 1);
+            s_tag[p] = v.tag; s_a[p] = v.a; s_b[p] = v.b; s_c[p] = v.c;
+        }
+    }
+    __syncthreads();
+
+    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0;
+    const Rec* recs = (const Rec*)a.rec;
+    const uint32_t end = start + cnt;
+    for (uint32_t gb = start; gb < end; gb += kRegionThreads) {
+        const uint32_t j = gb + t;
+        const bool valid = j < end;
+        Req q{};
+        if (valid) q = Codec::dec(recs[j], base);
+        const bool live = valid && !q.invalid;
+        if (valid && q.invalid) {
+            a.res[j] = pack_result(false, kRemInvalid);
+            if (a.tok) a.tok[j] = __builtin_nan("");
+            ++n_invalid;
+        }
+        // ---- find or insert the key's slot
+        int32_t slot = -1;
+        bool need = live, failed = false;
+        const uint32_t home = (uint32_t)q.h & (R - 1);
+        for (;;) {
+            uint32_t cand = kNone;
+            if (need) {
+                uint32_t p = home;
+                for (uint32_t step = 0; step < R; ++step) {
+                    if ((s_occ[p] & 1u) == 0u) { cand = p; break; }
+                    if (s_tag[p] == q.h) { slot = (int32_t)p; need = false; break; }
+                    p = (p + 1) & (R - 1);
+                }
+                if (need && cand == kNone) { need = false; failed = true; }
+            }
+            __syncthreads();
+            if (need && atomicCAS(&s_occ[cand], 0u, 1u) == 0u) {
+                s_tag[cand] = q.h; s_a[cand] = 0; s_b[cand] = 0; s_c[cand] = 0;
+                slot = (int32_t)cand;
+                need = false;
+            }
+            __syncthreads();
+            if (!__syncthreads_or(need)) break;
+        }
+        if (failed) {
+            a.res[j] = pack_result(false, kRemError);
+            if (a.tok) a.tok[j] = __builtin_nan("");
+            ++n_caperr;
+        }
+        if (slot >= 0) atomicOr(&s_occ[slot], 2u);
+        // ---- apply in arrival order: per round, the first state-changing request of
+        // each key applies; every earlier (non-mutating) request of that key is final.
+        bool pending = slot >= 0;
+        for (;;) {
+            Outcome o;
+            if (pending) {
+                o = tb ? tb_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot])
+                       : sw_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot]);
+                if (o.mutate) atomicMin(&s_fm[slot], t);
+            }
+            __syncthreads();
+            bool mine = false;
+            if (pending) {
+                const uint32_t fm = s_fm[slot];
+                if (t <= fm) {
+                    if (t == fm) {
+                        s_a[slot] = o.a; s_b[slot] = o.b; s_c[slot] = o.c;
+                        mine = true;
+                    }
+                    a.res[j] = pack_result(o.allowed, o.remaining);
+                    if (a.tok) a.tok[j] = o.tokens;
+                    n_allowed += o.allowed ? 1u : 0u;
+                    pending = false;
+                }
+            }
+            __syncthreads();
+            if (mine) s_fm[slot] = kNone;
+            if (!__syncthreads_or(pending)) break;
+        }
+    }
+    __syncthreads();
+    // ---- write the region back (free slots as zeros)
+    uint32_t touched = 0;
+    for (uint32_t s = t; s < R; s += kRegionThreads) {
+        const uint32_t o = s_occ[s];
+        Slot v;
+        if (o & 1u) { v.tag = s_tag[s]; v.a = s_a[s]; v.b = s_b[s]; v.c = s_c[s]; }
+        else { v.tag = 0; v.a = 0; v.b = 0; v.c = 0; }
+        tab[s] = v;
+        touched += (o >> 1) & 1u;
+    }
+    atomicAdd(&s_stat[0], n_allowed);
+    atomicAdd(&s_stat[1], n_invalid);
+    atomicAdd(&s_stat[2], n_caperr);
+    atomicAdd(&s_stat[3], touched);
+    __syncthreads();
+    if (t == 0) {
+        atomicAdd(&a.ctl->allowed, (unsigned long long)s_stat[0]);
+        atomicAdd(&a.ctl->invalid, (unsigned long long)s_stat[1]);
+        atomicAdd(&a.ctl->cap_err, (unsigned long long)s_stat[2]);
+        atomicAdd(&a.ctl->distinct, (unsigned long long)s_stat[3]);
+        atomicAdd(&a.ctl->regions, 1ULL);
+    }
+}
+
+// ------------------------------------------------------------------ 5. unpermute
+__global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
+    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t t = threadIdx.x;
+    for (int r = 0; r < kTileItems; ++r) {
+        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        if (i >= a.n) break;
+        uint32_t p = a.pos0[i];
+        if (a.pos1) p = a.pos1[p];
+        const uint64_t v = a.res[p];
+        a.allowed[i] = (uint8_t)(v & 1u);
+        a.remaining[i] = (int64_t)v >> 1;
+        if (a.tokens_out) a.tokens_out[i] = a.tok ? a.tok[p] : __builtin_nan("");
+    }
+}
+
+__global__ void k_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        allowed[i] = 0;
+        remaining[i] = kRemInvalid;
+        if (tok) tok[i] = __builtin_nan("");
+    }
+}
+
+// ------------------------------------------------------------------ synthetic traces
+// Deterministic in (seed, global index). Zipf via rejection-inversion (Hoermann &
+// Derflinger 1996, as in Apache Commons RejectionInversionZipfSampler).
+__device__ inline uint64_t splitmix(uint64_t x) { return mix64(x + 0x9E3779B97F4A7C15ULL); }
+__device__ inline double u01(uint64_t x) { return (double)(splitmix(x) >> 11) * 0x1.0p-53; }
+__device__ inline double zh1(double x) { return fabs(x) > 1e-8 ? log1p(x) / x : 1.0 - x * (0.5 - x / 3.0); }
+__device__ inline double zh2(double x) { return fabs(x) > 1e-8 ? expm1(x) / x : 1.0 + x * 0.5 * (1.0 + x / 3.0); }
+__device__ inline double zH(double x, double s) { const double lx = log(x); return zh2((1.0 - s) * lx) * lx; }
+__device__ inline double zh(double x, double s) { return exp(-s * log(x)); }
+__device__ inline double zHinv(double x, double s) {
+    double t = x * (1.0 - s);
+    if (t < -1.0) t = -1.0;
+    return exp(zh1(t) * x);
+}
+
+__global__ __launch_bounds__(256) void k_synth(SynthArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint64_t gi = a.index_base + i;
+    const uint64_t sd = a.seed * 0xD1B54A32D192ED03ULL;
+    uint64_t rank;
+    if (a.dist == 0) {
+        rank = splitmix(sd ^ (gi * 0x9E3779B97F4A7C15ULL)) % a.n_keys;
+    } else {
+        const double n = (double)a.n_keys;
+        uint64_t k = 1;
+        for (uint32_t att = 0; att < 64; ++att) {
+            const double u = a.hn + u01(sd ^ (gi * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)att << 56)) *
+                                        (a.hx1 - a.hn);
+            const double x = zHinv(u, a.zs);
+            double kd = floor(x + 0.5);
+            if (kd < 1.0) kd = 1.0;
+            if (kd > n) kd = n;
+            k = (uint64_t)kd;
+            if (kd - x <= a.sconst || u >= zH(kd + 0.5, a.zs) - zh(kd, a.zs)) break;
+        }
+        rank = k - 1;
+    }
+    a.key[i] = mix64(rank ^ (a.seed << 32) ^ 0x5EEDULL);
+    const uint64_t r2 = splitmix(sd ^ (gi * 0xA24BAED4963EE407ULL) ^ 0x77ULL);
+    a.permits[i] = 1 + (int32_t)(r2 % (uint64_t)a.permits_max);
+    a.now_ns[i] = a.t0_ns + (int64_t)((double)gi * (double)a.span_ns / (double)a.n_total);
+    if (a.limiter) a.limiter[i] = (uint16_t)(rank % a.n_limiters);
+}
+
+// ------------------------------------------------------------------ owner partition
+// Stable partition of a batch by owner shard (multi-GPU routing). One block per
+// 16K tile computes per-tile counts (upsweep), the host-side scan is done by
+// k_scan_rows, and the same tile re-ranks stably (shard_count <= 64).
+__global__ __launch_bounds__(kTileThreads) void k_owner_count(const uint64_t* key, uint32_t n,
+                                                              int sbits, uint32_t n_tiles,
+                                                              uint32_t* counts) {
+    __shared__ uint32_t hist[64];
+    const uint32_t t = threadIdx.x;
+    if (t < 64) hist[t] = 0;
+    __syncthreads();
+    const uint32_t tile = blockIdx.x;
+    for (int r = 0; r < kTileItems; ++r) {
+        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        if (i < n) {
+            const uint32_t o = sbits ? (uint32_t)(mix64(key[i]) >> (64 - sbits)) : 0u;
+            atomicAdd(&hist[o], 1u);
+        }
+    }
+    __syncthreads();
+    if (t < (1u << sbits)) counts[(size_t)t * n_tiles + tile] = hist[t];
+}
+
+__global__ __launch_bounds__(kTileThreads) void k_owner_scatter(const uint64_t* key, uint32_t n,
+                                                                int sbits, uint32_t n_tiles,
+                                                                const uint32_t* counts,
+                                                                const uint32_t* bin_base,
+                                                                uint32_t* perm) {
+    __shared__ uint32_t cur[64];
+    __shared__ uint8_t cntw[kTileThreads / 64][64];
+    const uint32_t t = threadIdx.x, wid = t >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t bins = 1u << sbits;
+    if (t < bins) {
+        cur[t] = bin_base[t] + counts[(size_t)t * n_tiles + tile];
+        for (int w = 0; w < kTileThreads / 64; ++w) cntw[w][t] = 0;
+    }
+    __syncthreads();
+    for (int r = 0; r < kTileItems; ++r) {
+        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        const bool active = i < n;
+        const uint32_t d = (active && sbits) ? (uint32_t)(mix64(key[i]) >> (64 - sbits)) : 0u;
+        const uint64_t m = wave_match(d, sbits, active);
+        const uint32_t lr = popc_below(m);
+        const uint32_t c = (uint32_t)__popcll(m);
+        const bool leader = active && lr == 0;
+        if (leader) cntw[wid][d] = (uint8_t)c;
+        __syncthreads();
+        uint32_t pos = 0;
+        if (active) {
+            pos = cur[d] + lr;
+            for (uint32_t w = 0; w < wid; ++w) pos += cntw[w][d];
+        }
+        __syncthreads();
+        if (leader) { atomicAdd(&cur[d], c); cntw[wid][d] = 0; }
+        if (active) perm[pos] = i;
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+static inline uint32_t tiles_for(uint32_t n) { return (n + kTile - 1) / kTile; }
+
+hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
+    dim3 grid(a.n_tiles), block(kTileThreads);
+    if (raw) {
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, true>), grid, block, 0, s, a);
+    } else {
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
+    dim3 grid(a.n_tiles), block(kTileThreads);
+    if (raw) {
+        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, 0, s, a);
+    } else {
+        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_scatter<CodecC, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, uint32_t cols,
+                            uint32_t* totals, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_rows, dim3(rows), dim3(256), 0, s, in, out, cols, totals);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, in, out, len);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
+                           uint32_t cols, hipStream_t s) {
+    hipLaunchKernelGGL(k_add_rows, dim3(rows), dim3(256), 0, s, row_base, data, cols);
+    return hipGetLastError();
+}
+
+hipError_t launch_region(const RegionArgs& a, bool wide, hipStream_t s) {
+    if (wide) hipLaunchKernelGGL((k_region<CodecW>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
+    else hipLaunchKernelGGL((k_region<CodecC>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpermute(const UnpermArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_unpermute, dim3(a.n_tiles), dim3(kTileThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_fill_invalid, dim3((n + 255) / 256), dim3(256), 0, s, allowed,
+                       remaining, tok, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(const SynthArgs& a, hipStream_t s) {
+    const uint64_t blocks = (a.n + 255) / 256;
+    hipLaunchKernelGGL(k_synth, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_owner_partition(const uint64_t* key, uint32_t n, uint32_t shard_count,
+                                  uint32_t* perm, uint32_t* counts_dev, uint32_t* scratch,
+                                  hipStream_t s) {
+    int sbits = 0;
+    while ((1u << sbits) < shard_count) ++sbits;
+    const uint32_t nt = tiles_for(n);
+    uint32_t* counts = scratch;                       // [shards][tiles]
+    uint32_t* base = scratch + (size_t)shard_count * nt;
+    hipLaunchKernelGGL(k_owner_count, dim3(nt), dim3(kTileThreads), 0, s, key, n, sbits, nt, counts);
+    hipLaunchKernelGGL(k_scan_rows, dim3(shard_count), dim3(256), 0, s, counts, counts, nt, counts_dev);
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, counts_dev, base, shard_count);
+    hipLaunchKernelGGL(k_owner_scatter, dim3(nt), dim3(kTileThreads), 0, s, key, n, sbits, nt,
+                       counts, base, perm);
+    return hipGetLastError();
+}
+
+}  // namespace rl

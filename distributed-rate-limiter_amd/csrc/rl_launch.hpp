@@ -1,0 +1,107 @@
+// rl_launch.hpp — host-side launchers for the kernels in rl_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_device.hpp"
+
+namespace rl {
+
+// Per-batch device control block (written by kernels, read by later kernels/host).
+struct BatchCtl {
+    int64_t base_ms;           // compact records: now_ms = base_ms + now_rel
+    uint64_t min_now_key;      // ordered-unsigned encoding of min now_ms
+    uint64_t max_now_key;
+    uint32_t span_overflow;    // compact: some now_ms outside [base, base + 2^32)
+    uint32_t pad;
+    unsigned long long allowed;
+    unsigned long long distinct;
+    unsigned long long invalid;
+    unsigned long long cap_err;
+    unsigned long long regions;
+};
+
+struct PartArgs {
+    // pass 0 reads the caller's SoA request arrays
+    const uint64_t* key;
+    const int32_t* permits;
+    const int64_t* now_ns;
+    const uint16_t* limiter;   // nullable
+    const uint8_t* op;         // nullable
+    // later passes read records
+    const void* rec_in;
+    void* rec_out;
+    uint32_t* pos_out;         // pos_out[i] = destination of element i
+    uint32_t n;
+    uint32_t n_tiles;
+    uint32_t n_lim;
+    int32_t shard_bits;
+    const DevLimiter* lims;
+    int32_t digit_shift;
+    int32_t digit_bits;
+    uint32_t* counts;          // [bins][n_tiles]: per-tile histogram, then exclusive row scan
+    const uint32_t* bin_base;  // [bins]
+    uint32_t* region_count;    // nullable: full-region histogram (multi-pass only)
+    BatchCtl* ctl;
+};
+
+struct RegionArgs {
+    const void* rec;           // records in region order
+    const uint32_t* rstart;    // [P]
+    const uint32_t* rcount;    // [P]
+    const uint8_t* region_lim; // [P]
+    const DevLimiter* lims;
+    uint64_t* res;             // packed results in region order
+    double* tok;               // nullable: TB fp64 balances in region order
+    BatchCtl* ctl;
+    uint32_t n_regions;
+};
+
+struct UnpermArgs {
+    const uint32_t* pos0;
+    const uint32_t* pos1;      // nullable
+    const uint64_t* res;
+    const double* tok;         // nullable
+    uint8_t* allowed;
+    int64_t* remaining;
+    double* tokens_out;        // nullable
+    uint32_t n;
+    uint32_t n_tiles;
+};
+
+struct SynthArgs {
+    uint64_t seed;
+    uint64_t n_keys;
+    int32_t dist;
+    int32_t permits_max;
+    int64_t t0_ns;
+    int64_t span_ns;
+    uint64_t index_base;
+    uint64_t n_total;
+    uint32_t n_limiters;
+    // Zipf rejection-inversion constants (host-computed)
+    double zs, hx1, hn, sconst;
+    uint64_t* key;
+    int32_t* permits;
+    int64_t* now_ns;
+    uint16_t* limiter;
+    uint64_t n;
+};
+
+hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s);
+hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s);
+hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, uint32_t cols,
+                            uint32_t* totals, hipStream_t s);
+hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hipStream_t s);
+hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
+                           uint32_t cols, hipStream_t s);
+hipError_t launch_region(const RegionArgs& a, bool wide, hipStream_t s);
+hipError_t launch_unpermute(const UnpermArgs& a, hipStream_t s);
+hipError_t launch_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n,
+                               hipStream_t s);
+hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
+hipError_t launch_owner_partition(const uint64_t* key, uint32_t n, uint32_t shard_count,
+                                  uint32_t* perm, uint32_t* counts_dev, uint32_t* scratch,
+                                  hipStream_t s);
+
+}  // namespace rl

@@ -1,0 +1,285 @@
+"""ctypes binding of librl_engine.so (include/rl_engine.h) for tests and bench.py.
+
+This is plumbing around the C-ABI: every decision is made by the HIP kernels in
+librl_engine.so. There is no CPU fallback — if the library is missing or no GPU is
+present, constructing an Engine raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "librl_engine.so")
+HEADER = os.path.join(REPO, "include", "rl_engine.h")
+
+RL_OK = 0
+RL_E_INVALID_ARG = -1
+RL_E_INVALID_REQUEST = -2
+RL_E_CAPACITY = -3
+RL_E_DEVICE = -4
+RL_E_NOMEM = -5
+RL_E_TOO_LARGE = -6
+RL_E_LIMITERS = -7
+
+SW, TB = 0, 1
+OP_ACQUIRE, OP_PEEK, OP_RESET = 0, 1, 2
+REM_UNKNOWN, REM_INVALID, REM_ERROR = -1, -2, -3
+OPT_STAGE_TIMING = 1
+DIST_UNIFORM, DIST_ZIPF = 0, 1
+
+EXPORTS = [
+    "rl_create", "rl_destroy", "rl_add_limiter", "rl_add_limiter_ex", "rl_try_acquire_batch",
+    "rl_execute_batch", "rl_execute_batch_device", "rl_last_status", "rl_available", "rl_reset",
+    "rl_batch_stats_get", "rl_stage_times", "rl_sync", "rl_strerror", "rl_abi_version",
+    "rl_owner_of", "rl_route_partition", "rl_synth_trace_device",
+]
+
+
+class RlError(RuntimeError):
+    def __init__(self, status, where=""):
+        self.status = status
+        super().__init__(f"{where}: {strerror(status)} ({status})")
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("max_batch", ctypes.c_uint64), ("default_capacity", ctypes.c_uint64),
+                ("shard_index", ctypes.c_uint32), ("shard_count", ctypes.c_uint32)]
+
+
+class LimiterConfig(ctypes.Structure):
+    _fields_ = [("algo", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("max_permits", ctypes.c_int64), ("window_ms", ctypes.c_int64),
+                ("refill_per_s", ctypes.c_double), ("capacity", ctypes.c_uint64)]
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("n", "allowed", "distinct_keys", "invalid",
+                                                 "capacity_errors", "regions_touched",
+                                                 "table_bytes")]
+
+
+class TraceSpec(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("n_keys", ctypes.c_uint64), ("dist", ctypes.c_int32),
+                ("permits_max", ctypes.c_int32), ("zipf_s", ctypes.c_double),
+                ("t0_ns", ctypes.c_int64), ("span_ns", ctypes.c_int64),
+                ("index_base", ctypes.c_uint64), ("n_total", ctypes.c_uint64),
+                ("n_limiters", ctypes.c_uint16), ("reserved", ctypes.c_uint16 * 3)]
+
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile librl_engine.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-j4", "-C", PKG_DIR])
+    else:
+        subprocess.check_call(["make", "-s", "-j4", "-C", PKG_DIR])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run `make -C {PKG_DIR}` (no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u16, u32, i32, i64, dbl = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint16,
+                                       ctypes.c_uint32, ctypes.c_int32, ctypes.c_int64,
+                                       ctypes.c_double)
+    L.rl_create.argtypes = [ctypes.POINTER(Opts), ctypes.POINTER(vp)]
+    L.rl_destroy.argtypes = [vp]
+    L.rl_destroy.restype = None
+    L.rl_add_limiter.argtypes = [vp, ctypes.c_int, i64, i64, dbl, ctypes.POINTER(u16)]
+    L.rl_add_limiter_ex.argtypes = [vp, ctypes.POINTER(LimiterConfig), ctypes.POINTER(u16)]
+    L.rl_try_acquire_batch.argtypes = [vp, sz] + [vp] * 7
+    L.rl_execute_batch.argtypes = [vp, sz] + [vp] * 8
+    L.rl_execute_batch_device.argtypes = [vp, sz] + [vp] * 9
+    L.rl_last_status.argtypes = [vp]
+    L.rl_available.argtypes = [vp, u16, sz, vp, vp, vp]
+    L.rl_reset.argtypes = [vp, u16, sz, vp, vp]
+    L.rl_batch_stats_get.argtypes = [vp, ctypes.POINTER(BatchStats)]
+    L.rl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p),
+                                 ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    L.rl_sync.argtypes = [vp]
+    L.rl_strerror.argtypes = [ctypes.c_int]
+    L.rl_strerror.restype = ctypes.c_char_p
+    L.rl_owner_of.argtypes = [ctypes.c_uint64, u16, u32]
+    L.rl_owner_of.restype = u32
+    L.rl_route_partition.argtypes = [vp, sz, vp, vp, u32, vp, vp, vp]
+    L.rl_synth_trace_device.argtypes = [vp, ctypes.POINTER(TraceSpec), sz, vp, vp, vp, vp, vp]
+    _lib = L
+    return L
+
+
+def strerror(status: int) -> str:
+    return lib().rl_strerror(int(status)).decode()
+
+
+def _p(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"]
+        return a.ctypes.data_as(ctypes.c_void_p)
+    if hasattr(a, "data_ptr"):          # torch tensor (device memory)
+        assert a.is_contiguous()
+        return ctypes.c_void_p(a.data_ptr())
+    return ctypes.c_void_p(int(a))
+
+
+def mix64(x):
+    """splitmix64 finaliser (the engine's key mixer), numpy uint64 vectorised."""
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(30))
+        x = x * np.uint64(0xBF58476D1CE4E5B9)
+        x = x ^ (x >> np.uint64(27))
+        x = x * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    return x
+
+
+def owner_of(keys, shard_count: int):
+    if shard_count <= 1:
+        return np.zeros(np.shape(keys), np.uint32)
+    s = int(shard_count).bit_length() - 1
+    return (mix64(keys) >> np.uint64(64 - s)).astype(np.uint32)
+
+
+class Engine:
+    """One engine = one GPU's state table + stream (rl_create)."""
+
+    def __init__(self, device: int = 0, max_batch: int = 1 << 22, capacity: int = 1 << 20,
+                 stage_timing: bool = False, shard_index: int = 0, shard_count: int = 1):
+        self._L = lib()
+        o = Opts(device=device, flags=OPT_STAGE_TIMING if stage_timing else 0,
+                 max_batch=max_batch, default_capacity=capacity, shard_index=shard_index,
+                 shard_count=shard_count)
+        h = ctypes.c_void_p()
+        st = self._L.rl_create(ctypes.byref(o), ctypes.byref(h))
+        if st != RL_OK:
+            raise RlError(st, "rl_create")
+        self._h = h
+        self.limiters = []
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.rl_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def add_limiter(self, algo, max_permits, window_ms, refill_per_s=0.0, capacity=0) -> int:
+        c = LimiterConfig(algo=int(algo), reserved=0, max_permits=int(max_permits),
+                          window_ms=int(window_ms), refill_per_s=float(refill_per_s),
+                          capacity=int(capacity))
+        lid = ctypes.c_uint16()
+        st = self._L.rl_add_limiter_ex(self._h, ctypes.byref(c), ctypes.byref(lid))
+        if st != RL_OK:
+            raise RlError(st, "rl_add_limiter")
+        self.limiters.append((algo, max_permits, window_ms, refill_per_s))
+        return lid.value
+
+    def execute(self, keys, permits, now_ns, limiter=None, ops=None, want_tokens=True):
+        """Host-buffer batch. Returns (allowed u8, remaining i64, tokens f64|None, status)."""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        permits = np.ascontiguousarray(permits, np.int32)
+        now_ns = np.ascontiguousarray(now_ns, np.int64)
+        limiter = None if limiter is None else np.ascontiguousarray(limiter, np.uint16)
+        ops = None if ops is None else np.ascontiguousarray(ops, np.uint8)
+        n = keys.shape[0]
+        allowed = np.zeros(n, np.uint8)
+        remaining = np.zeros(n, np.int64)
+        tokens = np.zeros(n, np.float64) if want_tokens else None
+        st = self._L.rl_execute_batch(self._h, n, _p(keys), _p(permits), _p(now_ns), _p(limiter),
+                                      _p(ops), _p(allowed), _p(remaining), _p(tokens))
+        if st in (RL_E_DEVICE, RL_E_NOMEM, RL_E_TOO_LARGE):
+            raise RlError(st, "rl_execute_batch")
+        return allowed, remaining, tokens, st
+
+    def try_acquire_batch(self, keys, permits, now_ns, limiter=None):
+        a, r, _, st = self.execute(keys, permits, now_ns, limiter, None, want_tokens=False)
+        return a, r, st
+
+    def execute_device(self, n, keys, permits, now_ns, limiter, ops, allowed, remaining,
+                       tokens=None, stream=None):
+        """Device-resident batch (torch tensors or raw device pointers); asynchronous."""
+        st = self._L.rl_execute_batch_device(self._h, n, _p(keys), _p(permits), _p(now_ns),
+                                             _p(limiter), _p(ops), _p(allowed), _p(remaining),
+                                             _p(tokens), _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_execute_batch_device")
+
+    def last_status(self) -> int:
+        return self._L.rl_last_status(self._h)
+
+    def available(self, limiter, keys, now_ns):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        now_ns = np.ascontiguousarray(now_ns, np.int64)
+        out = np.zeros(keys.shape[0], np.int64)
+        st = self._L.rl_available(self._h, int(limiter), keys.shape[0], _p(keys), _p(now_ns),
+                                  _p(out))
+        return out, st
+
+    def reset(self, limiter, keys, now_ns):
+        keys = np.ascontiguousarray(keys, np.uint64)
+        now_ns = np.ascontiguousarray(now_ns, np.int64)
+        return self._L.rl_reset(self._h, int(limiter), keys.shape[0], _p(keys), _p(now_ns))
+
+    def stats(self) -> dict:
+        s = BatchStats()
+        self._L.rl_batch_stats_get(self._h, ctypes.byref(s))
+        return {f: getattr(s, f) for f, _ in BatchStats._fields_}
+
+    def stage_times(self) -> dict:
+        names = (ctypes.c_char_p * 8)()
+        ms = (ctypes.c_float * 8)()
+        k = self._L.rl_stage_times(self._h, names, ms, 8)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+    def sync(self):
+        st = self._L.rl_sync(self._h)
+        if st != RL_OK:
+            raise RlError(st, "rl_sync")
+
+    def route_partition(self, n, keys_dev, perm_dev, shard_count, stream=None):
+        counts = np.zeros(shard_count, np.uint64)
+        st = self._L.rl_route_partition(self._h, n, _p(keys_dev), None, shard_count,
+                                        _p(perm_dev), _p(counts), _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_partition")
+        return counts
+
+    def synth_trace(self, n, keys, permits, now_ns, limiter, *, seed, n_keys, dist=DIST_UNIFORM,
+                    zipf_s=1.1, permits_max=4, t0_ns=1_700_000_000_000 * 1_000_000,
+                    span_ns=2_000_000_000, index_base=0, n_total=None, n_limiters=1,
+                    stream=None):
+        spec = TraceSpec(seed=seed, n_keys=n_keys, dist=dist, permits_max=permits_max,
+                         zipf_s=zipf_s, t0_ns=t0_ns, span_ns=span_ns, index_base=index_base,
+                         n_total=n_total or n, n_limiters=n_limiters)
+        st = self._L.rl_synth_trace_device(self._h, ctypes.byref(spec), n, _p(keys), _p(permits),
+                                           _p(now_ns), _p(limiter), _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_synth_trace_device")
