@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""bench.py — rate-limit decisions/s of the MI355X engine (BASELINE.json metric).
+
+A "step" is one batch of N timestamped requests, resident in HBM, pushed through the
+whole hot path (partition -> per-region sequential semantics -> results in caller
+order). Steps are consecutive slices of one synthetic trace, so state carries over
+and time moves forward exactly as in a replay.
+
+Default workload (N=1): BASELINE.json configs[1] — token bucket cap=50, refill=10/s,
+window 60 s (burstRateLimiter, RateLimiterConfig.java:88-92), 1M keys uniform,
+64M-request batches spanning 2 s each.
+
+Multi-GPU (torchrun, one rank per GPU): weak scaling. Every rank is a front-end that
+receives its own 64M-request slice of the global stream; requests are routed to the
+owner shard (top bits of mix64(key)) with RCCL all-to-all, decided there, and the
+decisions return by a second all-to-all.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "distributed-rate-limiter_amd", "python"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import rl_amd  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec per GPU
+NS = 1_000_000
+T0_NS = 1_700_000_000_000 * NS
+
+CONFIGS = {
+    # configs[1]: TB cap=50 refill=10/s, 1M keys uniform, 64M-request batch, 1 MI355X
+    "tb_uniform": dict(limiters=[(rl_amd.TB, 50, 60_000, 10.0)], n_keys=1_000_000,
+                       dist=rl_amd.DIST_UNIFORM, batch=1 << 26, span_ns=2_000 * NS,
+                       permits_max=4, seed=0x5EED0002, capacity=1_000_000,
+                       desc="TB cap=50 refill=10/s window=60s; 1M keys uniform; 64M-request "
+                            "batches over 2 s"),
+    # configs[2]: SW 1000/min, 100M keys Zipf s=1.1, 256M requests over 60 s
+    "sw_zipf": dict(limiters=[(rl_amd.SW, 1000, 60_000, 0.0)], n_keys=100_000_000,
+                    dist=rl_amd.DIST_ZIPF, zipf_s=1.1, batch=1 << 28, span_ns=60_000 * NS,
+                    permits_max=1, seed=0x5EED0003, capacity=30_000_000,
+                    desc="SW 1000/min window 60s; 100M keys Zipf s=1.1; 256M requests over 60 s"),
+}
+
+# algorithmic bytes per request / per distinct key
+REQ_BYTES = 22 + 9             # key 8 + now 8 + permits 4 + limiter 2 in; allowed 1 + remaining 8 out
+KEY_BYTES = 32 + 32            # state slot read + written
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def load_pmc(config_name, kernel):
+    """HBM traffic of the dominant kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        k = d.get(config_name, {}).get(kernel)
+        return None if k is None else float(k["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remaining):
+    from oracle.coracle import COracle
+    n = min(sample_n, keys.shape[0])
+    k = keys[:n].cpu().numpy().view(np.uint64)
+    p = permits[:n].cpu().numpy()
+    t = now[:n].cpu().numpy()
+    l = None if lim is None else lim[:n].cpu().numpy().view(np.uint16)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o1 = COracle(cfg["limiters"])
+    t0 = time.perf_counter()
+    a1, r1, _, _ = o1.run(k, p, t, l, None, want_tokens=False)
+    dt1 = time.perf_counter() - t0
+    o1.close()
+    oT = COracle(cfg["limiters"], nthreads=threads)
+    t0 = time.perf_counter()
+    aT, rT, _, _ = oT.run(k, p, t, l, None, want_tokens=False)
+    dtT = time.perf_counter() - t0
+    oT.close()
+    ga = gpu_allowed[:n]
+    gr = gpu_remaining[:n]
+    parity = bool(np.array_equal(ga, a1) and np.array_equal(gr, r1)
+                  and np.array_equal(aT, a1) and np.array_equal(rT, r1))
+    return {
+        "value": n / dtT, "unit": "decisions/s", "cores": threads, "kind": "port",
+        "sample": f"first {n} requests of batch 0 (same synthetic trace), oracle/rl_oracle.c "
+                  f"key-sharded over {threads} threads",
+        "single_thread_value": n / dt1,
+        "single_thread_seconds": dt1,
+        "sharded_seconds": dtT,
+    }, parity, n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="tb_uniform", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="requests per GPU per step (override)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    if ws != args.gpus and not (ws == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfg = CONFIGS[args.config]
+    n = args.batch or cfg["batch"]
+    steps, warm = args.steps, args.warmup
+    total_steps = steps + warm
+
+    eng = rl_amd.Engine(device=local, max_batch=n * (2 if ws > 1 else 1), capacity=cfg["capacity"],
+                        stage_timing=True, shard_index=rank, shard_count=ws)
+    for l in cfg["limiters"]:
+        eng.add_limiter(*l)
+
+    dev = torch.device("cuda", local)
+    n_global_total = total_steps * ws * n
+    inputs = []
+    for s in range(total_steps):
+        keys = torch.empty(n, dtype=torch.int64, device=dev)
+        permits = torch.empty(n, dtype=torch.int32, device=dev)
+        now = torch.empty(n, dtype=torch.int64, device=dev)
+        eng.synth_trace(n, keys, permits, now, None, seed=cfg["seed"], n_keys=cfg["n_keys"],
+                        dist=cfg["dist"], zipf_s=cfg.get("zipf_s", 1.1),
+                        permits_max=cfg["permits_max"], t0_ns=T0_NS,
+                        span_ns=cfg["span_ns"] * total_steps,
+                        index_base=(s * ws + rank) * n, n_total=n_global_total, n_limiters=1)
+        inputs.append((keys, permits, now))
+    allowed = torch.empty(n, dtype=torch.uint8, device=dev)
+    remaining = torch.empty(n, dtype=torch.int64, device=dev)
+    eng.sync()
+    torch.cuda.synchronize()
+
+    if ws > 1:
+        from rl_amd.router import Router
+        router = Router(eng, ws, rank, n, dev)
+
+        def step(s):
+            router.step(*inputs[s], allowed, remaining)
+    else:
+        def step(s):
+            k, p, t = inputs[s]
+            eng.execute_device(n, k, p, t, None, None, allowed, remaining)
+
+    keep0 = None
+    for s in range(warm):
+        step(s)
+        if s == 0:
+            eng.sync()
+            keep0 = (allowed.cpu().numpy(), remaining.cpu().numpy())
+    st = eng.last_status()
+    eng.stage_times()                      # drop warmup stage samples
+
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(warm, total_steps):
+        step(s)
+    eng.sync()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = eng.last_status()
+    stats = eng.stats()
+    stages = eng.stage_times()
+    ms_per_step = elapsed / steps * 1e3
+    value = ws * n * steps / elapsed
+
+    kern = {k: v for k, v in stages.items() if k != "total" and v > 0}
+    dom = max(kern, key=kern.get)
+    U = stats["distinct_keys"]
+    algo_bytes = n * REQ_BYTES + U * KEY_BYTES
+    achieved = algo_bytes / (kern[dom] * 1e-3) / 1e9
+    step_gbs = algo_bytes * ws / (elapsed / steps) / 1e9
+    traffic = load_pmc(args.config, dom)
+
+    out = {
+        "metric": "rate-limit decisions/sec (whole node)",
+        "value": value,
+        "unit": "decisions/s",
+        "n_gpus": ws,
+        "steps": steps,
+        "warmup": warm,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64" if cfg["limiters"][0][0] == rl_amd.TB else "int64+f64",
+        "data": "synthetic (deterministic splitmix64 trace generated on device)",
+        "config": {"workload": f"{args.config}: {cfg['desc']}", "requests_per_gpu_per_step": n,
+                   "n_keys": cfg["n_keys"], "parallelism": f"key-hash shards x{ws}"
+                   + (" + RCCL all-to-all routing" if ws > 1 else "")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom,
+                     "kernel_ms": kern[dom],
+                     "algorithmic_bytes_per_launch": algo_bytes,
+                     "step_frac": step_gbs / (HBM_PEAK_GBS * ws)},
+        "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+        "batch_stats": {k: stats[k] for k in ("allowed", "distinct_keys", "invalid",
+                                              "capacity_errors", "regions_touched")},
+        "status": rl_amd.strerror(st),
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        k0, p0, t0_ = inputs[0]
+        cb, parity, m = cpu_baseline(cfg, k0, p0, t0_, None, args.cpu_sample, keep0[0], keep0[1])
+        out["cpu_baseline"] = cb
+        out["parity"] = f"{'bit-exact' if parity else 'MISMATCH'} vs oracle on the first {m} " \
+                        f"requests of batch 0"
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out))
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,9 +21,15 @@ using namespace rl;
 
 namespace {
 
-constexpr int kStages = 6;
-const char* kStageNames[kStages] = {"partition0", "partition1", "region_offsets", "region",
-                                    "unpermute", "total"};
+// Stage timing: events bracket every kernel of a batch; a ring of per-batch event
+// sets is averaged when rl_stage_times is called (no host sync inside a batch).
+constexpr int kMarks = 10;   // marks 0..9
+constexpr int kStages = 10;
+const char* kStageNames[kStages] = {"upsweep0", "scan0", "scatter0", "upsweep1", "scan1",
+                                    "scatter1", "region_offsets", "region", "unpermute", "total"};
+const int kStagePairs[kStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6},
+                                     {6, 7}, {7, 8}, {8, 9}, {0, 9}};
+constexpr int kRing = 64;
 
 struct HostLimiter {
     rl_limiter_config cfg;
@@ -90,8 +96,9 @@ struct rl_engine {
     size_t route_cap = 0;
     uint32_t* route_counts = nullptr;
 
-    hipEvent_t ev[kStages + 1] = {};
-    float stage_ms[kStages] = {};
+    hipEvent_t ev[kRing][kMarks] = {};
+    int ring_used = 0;                      // batches recorded since the last query
+    int ring_next = 0;
     bool timing = false;
     bool last_wide = false;
     bool pending_status = false;
@@ -179,7 +186,9 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
         return RL_E_DEVICE;
     }
     e->timing = (o.flags & RL_OPT_STAGE_TIMING) != 0;
-    for (int i = 0; i <= kStages; ++i) (void)hipEventCreate(&e->ev[i]);
+    if (e->timing)
+        for (int r = 0; r < kRing; ++r)
+            for (int i = 0; i < kMarks; ++i) (void)hipEventCreate(&e->ev[r][i]);
     int rc = dalloc(&e->d_ctl, 1);
     if (rc == RL_OK && hipHostMalloc((void**)&e->h_ctl, sizeof(BatchCtl)) != hipSuccess) rc = RL_E_NOMEM;
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
@@ -204,7 +213,8 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
     dfree(e->route_scratch); dfree(e->route_counts);
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
-    for (int i = 0; i <= kStages; ++i) if (e->ev[i]) (void)hipEventDestroy(e->ev[i]);
+    for (int r = 0; r < kRing; ++r)
+        for (int i = 0; i < kMarks; ++i) if (e->ev[r][i]) (void)hipEventDestroy(e->ev[r][i]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -321,7 +331,7 @@ static int ensure_regions(rl_engine* e, size_t padded) {
 }
 
 static inline void mark(rl_engine* e, int i) {
-    if (e->timing) (void)hipEventRecord(e->ev[i], e->stream);
+    if (e->timing) (void)hipEventRecord(e->ev[e->ring_next][i], e->stream);
 }
 
 // The pipeline on device buffers, enqueued on e->stream. Returns an immediate status
@@ -374,10 +384,12 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     pa.rec_out = e->rec0; pa.pos_out = e->pos0;
     HIP_OK(launch_upsweep(pa, true, wide, s));
+    mark(e, 1);
     HIP_OK(launch_scan_rows(e->counts, e->counts, 1u << d0, nt, e->bin_total, s));
     HIP_OK(launch_scan_small(e->bin_total, e->bin_base, 1u << d0, s));
+    mark(e, 2);
     HIP_OK(launch_scatter(pa, true, wide, s));
-    mark(e, 1);
+    mark(e, 3);
     const void* rec_final = e->rec0;
     const uint32_t* rstart = e->bin_base;
     const uint32_t* rcount = e->bin_total;
@@ -388,12 +400,17 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         pa.digit_shift = d0; pa.digit_bits = d1;
         pa.rec_in = e->rec0; pa.rec_out = e->rec1; pa.pos_out = e->pos1;
         HIP_OK(launch_upsweep(pa, false, wide, s));
+        mark(e, 4);
         HIP_OK(launch_scan_rows(e->counts, e->counts, 1u << d1, nt, e->bin_total, s));
         HIP_OK(launch_scan_small(e->bin_total, e->bin_base, 1u << d1, s));
+        mark(e, 5);
         HIP_OK(launch_scatter(pa, false, wide, s));
         rec_final = e->rec1;
+    } else {
+        mark(e, 4);
+        mark(e, 5);
     }
-    mark(e, 2);
+    mark(e, 6);
     if (passes == 2) {
         const uint32_t rows = (uint32_t)(padded / cols);
         HIP_OK(launch_scan_rows(e->region_count, e->region_start, rows, cols, e->row_tmp, s));
@@ -402,20 +419,24 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         rstart = e->region_start;
         rcount = e->region_count;
     }
-    mark(e, 3);
+    mark(e, 7);
     RegionArgs ra{};
     ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.region_lim = e->d_region_lim;
     ra.lims = e->d_lims; ra.res = e->res; ra.tok = tokens_after ? e->tok : nullptr;
     ra.ctl = e->d_ctl; ra.n_regions = e->n_regions;
     HIP_OK(launch_region(ra, wide, s));
-    mark(e, 4);
+    mark(e, 8);
     UnpermArgs ua{};
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
     ua.tok = tokens_after ? e->tok : nullptr;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
     ua.n = (uint32_t)n; ua.n_tiles = nt;
     HIP_OK(launch_unpermute(ua, s));
-    mark(e, 5);
+    mark(e, 9);
+    if (e->timing) {
+        e->ring_next = (e->ring_next + 1) % kRing;
+        e->ring_used = std::min(e->ring_used + 1, kRing);
+    }
     HIP_OK(hipMemcpyAsync(e->h_ctl, e->d_ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, s));
     e->pending_status = true;
     return RL_OK;
@@ -425,13 +446,6 @@ static int collect_status(rl_engine* e) {
     HIP_OK(hipStreamSynchronize(e->stream));
     if (!e->pending_status) return e->last_status;
     e->pending_status = false;
-    if (e->timing) {
-        float ms;
-        const int pairs[kStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {0, 5}};
-        for (int i = 0; i < kStages; ++i) {
-            e->stage_ms[i] = hipEventElapsedTime(&ms, e->ev[pairs[i][0]], e->ev[pairs[i][1]]) == hipSuccess ? ms : -1.f;
-        }
-    }
     const BatchCtl& c = *e->h_ctl;
     int st = RL_OK;
     if (c.invalid) st = RL_E_INVALID_REQUEST;
@@ -567,15 +581,27 @@ extern "C" int rl_batch_stats_get(rl_engine* e, rl_batch_stats* out) {
     return RL_OK;
 }
 
+// Average per-stage milliseconds over the batches enqueued since the previous call
+// (at most the last 64). Stages a batch did not run (second pass) read 0.
 extern "C" int rl_stage_times(rl_engine* e, const char** names, float* ms, int cap) {
     if (!e) return RL_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(e->mu);
     collect_status(e);
-    int k = std::min(cap, kStages);
+    const int k = std::min(cap, kStages);
+    const int nb = e->ring_used;
     for (int i = 0; i < k; ++i) {
+        double acc = 0.0;
+        for (int b = 0; b < nb; ++b) {
+            const int r = (e->ring_next - 1 - b + kRing) % kRing;
+            float x = 0.f;
+            if (hipEventElapsedTime(&x, e->ev[r][kStagePairs[i][0]], e->ev[r][kStagePairs[i][1]]) != hipSuccess)
+                x = 0.f;
+            acc += x;
+        }
         if (names) names[i] = kStageNames[i];
-        if (ms) ms[i] = e->timing ? e->stage_ms[i] : -1.f;
+        if (ms) ms[i] = (e->timing && nb) ? (float)(acc / nb) : -1.f;
     }
+    e->ring_used = 0;
     return k;
 }
 

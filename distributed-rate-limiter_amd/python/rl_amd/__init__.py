@@ -88,6 +88,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # torch (ROCm) ships its own libamdhip64.so.7; the engine links the same soname. Load
+    # torch first so both share ONE HIP runtime in this process (device pointers from torch
+    # tensors are then valid for the engine and torch can still initialise afterwards).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: run `make -C {PKG_DIR}` (no CPU fallback)")
     L = ctypes.CDLL(LIB_PATH)
@@ -254,9 +261,9 @@ class Engine:
         return {f: getattr(s, f) for f, _ in BatchStats._fields_}
 
     def stage_times(self) -> dict:
-        names = (ctypes.c_char_p * 8)()
-        ms = (ctypes.c_float * 8)()
-        k = self._L.rl_stage_times(self._h, names, ms, 8)
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        k = self._L.rl_stage_times(self._h, names, ms, 16)
         return {names[i].decode(): float(ms[i]) for i in range(k)}
 
     def sync(self):
