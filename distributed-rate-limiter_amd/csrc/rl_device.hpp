@@ -26,16 +26,19 @@ constexpr int64_t kRemInvalid = -2;   // permits <= 0 / unknown limiter
 constexpr int64_t kRemError = -3;     // state-table region full
 
 // State table: a limiter's keys live in 2^k regions of kRegionSlots slots. One
-// workgroup owns a region for a whole batch, so a region needs no atomics in HBM.
-constexpr int kRegionSlots = 512;                 // slots per region (load <= ~0.5)
-constexpr int kRegionThreads = 256;               // workgroup of the region kernel
+// wavefront owns a region for a whole batch (its 8 KB image lives in that wave's
+// LDS), so a region needs no atomics in HBM and no workgroup barriers.
+constexpr int kRegionSlots = 256;                 // slots per region (load <= ~0.5)
+constexpr int kRegionBits = 8;
+constexpr int kRegionThreads = 64;                // one wave per region
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-// Partition tiles (upsweep / scatter / unpermute all share this tiling).
+// Partition tiles (upsweep / scatter / unpermute all share this tiling). 64K
+// requests per tile: with <= 8192 bins a tile writes >= 8 records (128 B) per bin.
 constexpr int kTileThreads = 256;
-constexpr int kTileItems = 64;
-constexpr int kTile = kTileThreads * kTileItems;  // 16384 requests per tile
-constexpr int kMaxDigitBits = 12;                 // <= 4096 bins per pass
+constexpr int kTileItems = 256;
+constexpr int kTile = kTileThreads * kTileItems;  // 65536 requests per tile
+constexpr int kMaxDigitBits = 13;                 // <= 8192 bins per pass
 
 // Compact record field limits.
 constexpr uint32_t kPermitBits = 22;
@@ -109,6 +112,7 @@ struct Req {                 // decoded request
 
 struct CodecC {
     using Rec = RecC;
+    using Res = uint32_t;
     __device__ static inline Rec enc(uint64_t h, int64_t now_ms, int64_t base, int32_t permits,
                                      uint32_t op, uint32_t lim, bool invalid) {
         Rec r;
@@ -137,6 +141,7 @@ struct CodecC {
 
 struct CodecW {
     using Rec = RecW;
+    using Res = uint64_t;
     __device__ static inline Rec enc(uint64_t h, int64_t now_ms, int64_t, int32_t permits,
                                      uint32_t op, uint32_t lim, bool invalid) {
         Rec r;
@@ -154,9 +159,20 @@ struct CodecW {
 };
 
 // ---------------------------------------------------------------- results
-// Packed 8-byte result in partition order: remaining << 1 | allowed.
+// Packed result in partition order: (remaining + 3) << 1 | allowed (remaining >= -3).
+// The width is the narrowest that holds every limiter's max_permits: u8 (max <= 124),
+// u16 (max <= 32764), u32 (compact records), u64 (wide records). Rate limits are
+// usually small, so the result array is 1-2 bytes per request and stays in the
+// 256 MiB Infinity Cache for the unpermute gather.
+constexpr int64_t kResBias = 3;
 __device__ inline uint64_t pack_result(bool allowed, int64_t remaining) {
-    return ((uint64_t)remaining << 1) | (allowed ? 1u : 0u);
+    return ((uint64_t)(remaining + kResBias) << 1) | (allowed ? 1u : 0u);
+}
+__host__ __device__ inline int res_bytes_for(int64_t max_permits, bool wide) {
+    if (wide) return 8;
+    if ((max_permits + kResBias) * 2 + 1 < 256) return 1;
+    if ((max_permits + kResBias) * 2 + 1 < 65536) return 2;
+    return 4;
 }
 
 // Java (long) narrowing of a double (JLS 5.1.3) / Redis (long long) of a Lua number.
@@ -245,15 +261,41 @@ __device__ inline int64_t sw_get(const SW2& s, int64_t start, int64_t now, int64
     return 0;
 }
 
+// Java long division / remainder (truncating) by 0 < w < 2^31, exact for |a| < 2^53:
+// a correctly rounded fp64 quotient is within 1 of the true one; fix it up in integers.
+__device__ inline int64_t jdiv(int64_t a, int64_t w, int64_t* rem) {
+    int64_t q = (int64_t)((double)a / (double)w);
+    int64_t r = a - q * w;
+    if (r < 0 && a >= 0) { q -= 1; r += w; }
+    else if (r >= w) { q += 1; r -= w; }
+    else if (r > 0 && a < 0) { q += 1; r -= w; }
+    else if (r <= -w) { q -= 1; r += w; }
+    *rem = r;
+    return q;
+}
+
+// Window geometry of a request (getWindowKey :185-188 for now and now - w).
+struct SWGeo {
+    int64_t curr_start, prev_start;
+    double prev_weight;      // 1.0 - (double)(now % w) / w   (:170-171)
+};
+
+__device__ inline SWGeo sw_geo(int64_t now, int64_t w) {
+    SWGeo g;
+    int64_t r, r2;
+    const int64_t q = jdiv(now, w, &r);
+    g.curr_start = q * w;
+    g.prev_start = jdiv(now - w, w, &r2) * w;
+    const double pct = (double)r / (double)w;
+    g.prev_weight = 1.0 - pct;
+    return g;
+}
+
 // getCurrentCount (SlidingWindowRateLimiter.java:158-180).
-__device__ inline int64_t sw_estimate(const SW2& s, int64_t now, int64_t w) {
-    const int64_t curr_start = (now / w) * w;                 // getWindowKey :186
-    const int64_t prev_start = ((now - w) / w) * w;
-    const int64_t curr = sw_get(s, curr_start, now, w);
-    const int64_t prev = sw_get(s, prev_start, now, w);
-    const double pct = (double)(now % w) / (double)w;         // :170
-    const double prev_weight = 1.0 - pct;                     // :171
-    const double t = (double)prev * prev_weight;              // :174, rounded
+__device__ inline int64_t sw_estimate(const SW2& s, const SWGeo& g, int64_t now, int64_t w) {
+    const int64_t curr = sw_get(s, g.curr_start, now, w);
+    const int64_t prev = sw_get(s, g.prev_start, now, w);
+    const double t = (double)prev * g.prev_weight;            // :174, rounded
     const double sum = t + (double)curr;                      //       rounded separately
     return d2l(sum);
 }
@@ -265,9 +307,10 @@ __device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t perm
     o.a = a; o.b = b; o.c = c;
     const int64_t w = L.window_ms;
     SW2 s = sw_unpack(a, b, c);
-    const int64_t curr_start = (now / w) * w;
+    const SWGeo geo = sw_geo(now, w);
+    const int64_t curr_start = geo.curr_start;
     if (op == (uint32_t)kOpReset) {                  // reset (:139-153): DEL curr and prev
-        const int64_t prev_start = ((now - w) / w) * w;
+        const int64_t prev_start = geo.prev_start;
         if (s.b1_start == curr_start || s.b1_start == prev_start) s.b1_cnt = 0;
         const int64_t b0_start = s.b1_start - w;
         if (b0_start == curr_start || b0_start == prev_start) s.b0_cnt = 0;
@@ -275,7 +318,7 @@ __device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t perm
         o.b = (uint64_t)s.b1_cnt | ((uint64_t)s.b0_cnt << 32);
         return o;
     }
-    const int64_t est = sw_estimate(s, now, w);
+    const int64_t est = sw_estimate(s, geo, now, w);
     if (op == (uint32_t)kOpPeek || est + (int64_t)permits > L.max_permits) {  // :104
         const int64_t r = L.max_permits - est;
         o.remaining = r > 0 ? r : 0;
@@ -294,7 +337,7 @@ __device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t perm
     s.b1_off = (int32_t)(now - curr_start);
     o.mutate = true;
     o.allowed = (int64_t)s.b1_cnt <= L.max_permits;  // :123
-    const int64_t est2 = sw_estimate(s, now, w);     // remaining after the request (A4)
+    const int64_t est2 = sw_estimate(s, geo, now, w);  // remaining after the request (A4)
     const int64_t r = L.max_permits - est2;
     o.remaining = r > 0 ? r : 0;
     o.a = (uint64_t)s.b1_start;

@@ -66,7 +66,7 @@ struct rl_engine {
     void* rec1 = nullptr;
     uint32_t* pos0 = nullptr;
     uint32_t* pos1 = nullptr;
-    uint64_t* res = nullptr;
+    void* res = nullptr;
     double* tok = nullptr;
     uint32_t* counts = nullptr;             // [bins][tiles]
     size_t counts_cap = 0;
@@ -296,13 +296,14 @@ static int ensure_scratch(rl_engine* e, size_t n, bool wide, uint32_t bins, uint
     if (n > e->cap_n || (wide && !e->cap_wide)) {
         size_t cap = std::max<size_t>(n, std::min<size_t>(e->opts.max_batch, std::max<size_t>(n, 1u << 20)));
         const size_t rb = wide ? sizeof(RecW) : sizeof(RecC);
+        const size_t padn = cap + kTileThreads;   // kernels write inactive lanes past n
         dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
-        int rc = dalloc(&e->rec0, cap * rb);
-        if (rc == RL_OK) rc = dalloc(&e->rec1, cap * rb);
-        if (rc == RL_OK) rc = dalloc(&e->pos0, cap);
-        if (rc == RL_OK) rc = dalloc(&e->pos1, cap);
-        if (rc == RL_OK) rc = dalloc(&e->res, cap);
-        if (rc == RL_OK) rc = dalloc(&e->tok, cap);
+        int rc = dalloc(&e->rec0, padn * rb);
+        if (rc == RL_OK) rc = dalloc(&e->rec1, padn * rb);
+        if (rc == RL_OK) rc = dalloc(&e->pos0, padn);
+        if (rc == RL_OK) rc = dalloc(&e->pos1, padn);
+        if (rc == RL_OK) rc = dalloc(&e->res, padn * sizeof(uint64_t));
+        if (rc == RL_OK) rc = dalloc(&e->tok, padn);
         if (rc != RL_OK) { e->cap_n = 0; return rc; }
         e->cap_n = cap;
         e->cap_wide = wide;
@@ -352,7 +353,12 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         return RL_OK;
     }
     bool wide = false;
-    for (auto& l : e->lims) wide |= l.cfg.max_permits > kCompactMaxPermits;
+    int64_t max_any = 0;
+    for (auto& l : e->lims) {
+        wide |= l.cfg.max_permits > kCompactMaxPermits;
+        max_any = std::max<int64_t>(max_any, l.cfg.max_permits);
+    }
+    const int res_bytes = res_bytes_for(max_any, wide);
     const uint32_t nt = (uint32_t)((n + kTile - 1) / kTile);
     const int bitsP = std::max(1, ceil_log2(e->n_regions));
     const int passes = bitsP <= kMaxDigitBits ? 1 : 2;
@@ -423,15 +429,15 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     RegionArgs ra{};
     ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.region_lim = e->d_region_lim;
     ra.lims = e->d_lims; ra.res = e->res; ra.tok = tokens_after ? e->tok : nullptr;
-    ra.ctl = e->d_ctl; ra.n_regions = e->n_regions;
-    HIP_OK(launch_region(ra, wide, s));
+    ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n;
+    HIP_OK(launch_region(ra, wide, res_bytes, s));
     mark(e, 8);
     UnpermArgs ua{};
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
     ua.tok = tokens_after ? e->tok : nullptr;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
     ua.n = (uint32_t)n; ua.n_tiles = nt;
-    HIP_OK(launch_unpermute(ua, s));
+    HIP_OK(launch_unpermute(ua, res_bytes, s));
     mark(e, 9);
     if (e->timing) {
         e->ring_next = (e->ring_next + 1) % kRing;

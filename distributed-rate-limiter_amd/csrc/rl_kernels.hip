@@ -3,22 +3,24 @@
 // One batch = requests in arrival order. The pipeline groups every request with
 // the other requests of its (limiter, key) WITHOUT a full sort:
 //
-//   1. k_upsweep  : per 16K-request tile, histogram of the partition digit of each
+//   1. k_upsweep  : per 64K-request tile, histogram of the partition digit of each
 //                   request's state-table REGION (region = top bits of mix64(key)).
 //   2. k_scan_rows/k_scan_small : exclusive scan of the [bin][tile] histogram.
 //   3. k_scatter  : stable partition (wave ballot-match ranking) of the requests
 //                   into region order, packed into 16-byte records.
-//   (2-3 repeat once more when a limiter set has > 4096 regions.)
-//   4. k_region   : one workgroup per region. Loads the region's 512 state slots
-//                   (16 KB) into LDS once, streams the region's records in arrival
-//                   order 256 at a time, applies the reference semantics per key in
-//                   order (deny never mutates, so a group needs 1 + (#state changes of
-//                   its busiest key) rounds), writes the region back once.
+//   (1-3 repeat once more when a limiter set has > 8192 regions.)
+//   4. k_region   : one WAVE per region. Loads the region's 256 state slots (8 KB)
+//                   into LDS once, streams the region's records in arrival order 64
+//                   at a time, applies the reference semantics per key in order (deny
+//                   never mutates, so a group needs 1 + (#state changes of its busiest
+//                   key) rounds), writes the region back once.
 //   5. k_unpermute: results back to the caller's order (allowed u8, remaining i64).
 //
 // Tiles are mapped XCD-aware (consecutive tiles on one XCD) so the per-tile
 // histogram columns, the record runs of one bin and the result gathers of
 // neighbouring tiles combine in that XCD's L2 instead of going to HBM as partial lines.
+#include <type_traits>
+
 #include "rl_launch.hpp"
 
 #pragma clang fp contract(off)
@@ -126,6 +128,7 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
     __syncthreads();
     const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
     const uint32_t mask = bins - 1;
+#pragma unroll 8
     for (int r = 0; r < kTileItems; ++r) {
         const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
         if (i < a.n) {
@@ -188,7 +191,32 @@ __global__ __launch_bounds__(256) void k_add_rows(const uint32_t* row_base, uint
 
 // ------------------------------------------------------------------ 3. scatter
 // Stable: a tile's elements are ranked in (round, wave, lane) order, which is the
-// arrival order; tiles are ordered by the exclusive [bin][tile] scan.
+// arrival order; tiles are ordered by the exclusive [bin][tile] scan. The inputs of
+// round r+1 are loaded into registers before round r is ranked, so the global-load
+// latency hides behind the two LDS barriers of a round.
+template <class Codec, bool RAW>
+struct ScatterIn;
+
+template <class Codec>
+struct ScatterIn<Codec, true> {
+    uint64_t key; int64_t now_ns; int32_t permits; uint32_t lim; uint32_t op;
+    __device__ inline void load(const PartArgs& a, uint32_t i) {
+        key = a.key[i];
+        now_ns = a.now_ns[i];
+        permits = a.permits[i];
+        lim = a.limiter ? a.limiter[i] : 0u;
+        op = a.op ? a.op[i] : 0u;
+    }
+};
+
+template <class Codec>
+struct ScatterIn<Codec, false> {
+    typename Codec::Rec rec;
+    __device__ inline void load(const PartArgs& a, uint32_t i) {
+        rec = ((const typename Codec::Rec*)a.rec_in)[i];
+    }
+};
+
 template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     using Rec = typename Codec::Rec;
@@ -199,6 +227,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t bins = 1u << a.digit_bits, mask = bins - 1;
     const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+    const uint32_t tile0 = tile * (uint32_t)kTile;
     for (uint32_t b = t; b < bins; b += kTileThreads) {
         cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
 #pragma unroll
@@ -207,26 +236,34 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     load_lim_lds(L, a);
     int64_t base = 0;
     if constexpr (RAW) base = a.ctl->base_ms;
+    // two rounds of inputs in flight; out-of-range lanes re-load element n-1 so every
+    // wave issues the same loads and stores each round (static vmcnt counting: the
+    // waits for round r+2's inputs never include round r's scattered stores).
+    const uint32_t last = a.n - 1;
+    ScatterIn<Codec, RAW> nx1, nx2;
+    nx1.load(a, min(tile0 + t, last));
+    nx2.load(a, min(tile0 + kTileThreads + t, last));
     __syncthreads();
     uint64_t mn = ~0ULL, mx = 0;
     bool overflow = false;
     for (int r = 0; r < kTileItems; ++r) {
-        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        const uint32_t i = tile0 + (uint32_t)r * kTileThreads + t;
         const bool active = i < a.n;
+        const ScatterIn<Codec, RAW> in = nx1;
+        nx1 = nx2;
+        nx2.load(a, min(i + 2 * kTileThreads, last));
         Rec rec{};
         uint32_t d = 0;
         if (active) {
             if constexpr (RAW) {
-                const uint64_t key = a.key[i];
-                uint32_t lim = a.limiter ? a.limiter[i] : 0u;
-                const int32_t p = a.permits[i];
-                const int64_t now_ms = floor_div_ms(a.now_ns[i]);
-                uint32_t op = a.op ? a.op[i] : 0u;
+                uint32_t lim = in.lim, op = in.op;
+                const int32_t p = in.permits;
+                const int64_t now_ms = floor_div_ms(in.now_ns);
                 const bool lim_ok = lim < a.n_lim;
                 if (!lim_ok) lim = 0;
                 const bool invalid = !lim_ok || op > 2u || (op == 0u && p <= 0);
                 if (op > 2u) op = 0;
-                const uint64_t h = mix64(key);
+                const uint64_t h = mix64(in.key);
                 rec = Codec::enc(h, now_ms, base, p, op, lim, invalid);
                 const int64_t rel = now_ms - base;
                 overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
@@ -235,7 +272,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                 mx = k > mx ? k : mx;
                 d = ((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.digit_shift) & mask;
             } else {
-                rec = ((const Rec*)a.rec_in)[i];
+                rec = in.rec;
                 const uint32_t lim = Codec::limiter_of(rec);
                 d = ((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.digit_shift) & mask;
             }
@@ -256,10 +293,10 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
             atomicAdd(&cur[d], cnt);
             cntw[wid][d] = 0;
         }
-        if (active) {
-            ((Rec*)a.rec_out)[pos] = rec;
-            a.pos_out[i] = pos;
-        }
+        // inactive lanes write to the padding slot past n (buffers carry 256 spare entries)
+        const uint32_t wpos = active ? pos : a.n + t;
+        ((Rec*)a.rec_out)[wpos] = rec;
+        a.pos_out[active ? i : a.n + t] = pos;
     }
     if constexpr (RAW) {
         // min / max now over the tile -> one atomic each
@@ -283,131 +320,128 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
 }
 
 // ------------------------------------------------------------------ 4. region
-template <class Codec>
+// One wavefront per region. The region's 256 slots (8 KB) are loaded into this
+// wave's LDS once, rebuilt without expired entries, the region's records are streamed
+// in arrival order 64 at a time, and the image is written back once. Everything is
+// wave-synchronous: no workgroup barriers, no HBM atomics.
+__device__ inline void wave_fence() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }
+
+template <class Codec, class Res, bool TOK>
 __global__ __launch_bounds__(kRegionThreads) void k_region(RegionArgs a) {
     using Rec = typename Codec::Rec;
-    constexpr uint32_t R = kRegionSlots;
-    __shared__ uint64_t s_tag[R], s_a[R], s_b[R], s_c[R];
-    __shared__ uint32_t s_occ[R];   // bit0 occupied, bit1 touched by this batch
-    __shared__ uint32_t s_fm[R];    // first mutating lane of the current round
-    __shared__ uint32_t s_stat[4];
+    constexpr uint32_t S = kRegionSlots;
+    __shared__ uint64_t s_tag[S], s_a[S], s_b[S], s_c[S];
+    __shared__ uint32_t s_occ[S];   // bit0 occupied, bit1 touched by this batch
 
     const uint32_t g = blockIdx.x;
     const uint32_t cnt = a.rcount[g];
     if (cnt == 0) return;
     const uint32_t start = a.rstart[g];
-    const uint32_t t = threadIdx.x;
+    const uint32_t end = start + cnt;
+    const uint32_t lane = threadIdx.x;
     const DevLimiter L = a.lims[a.region_lim[g]];
     const bool tb = L.algo == kAlgoTB;
-    const bool span_bad = a.ctl->span_overflow != 0;
     const int64_t base = a.ctl->base_ms;
     const int64_t batch_min = (int64_t)(a.ctl->min_now_key ^ 0x8000000000000000ULL);
-    Slot* tab = (Slot*)L.table + (size_t)(g - L.region_base) * R;
+    Res* res = (Res*)a.res;
+    const Rec* recs = (const Rec*)a.rec;
+    const uint32_t pad = a.n_total + lane;       // padding slot for lanes past `end`
 
-    for (uint32_t s = t; s < R; s += kRegionThreads) { s_occ[s] = 0; s_fm[s] = kNone; }
-    if (t < 4) s_stat[t] = 0;
-    __syncthreads();
-
-    if (span_bad) {
+    if (a.ctl->span_overflow != 0) {
         // compact records cannot represent this batch's time span: reject it whole,
         // before any state is touched (the host reports RL_E_INVALID_ARG).
-        for (uint32_t j = start + t; j < start + cnt; j += kRegionThreads) {
-            a.res[j] = pack_result(false, kRemInvalid);
-            if (a.tok) a.tok[j] = __builtin_nan("");
+        for (uint32_t j = start + lane; j < end; j += 64) {
+            res[j] = (Res)pack_result(false, kRemInvalid);
+            if (TOK) a.tok[j] = __builtin_nan("");
         }
         return;
     }
+    // prefetch the first group of records while the region image loads
+    Rec nxt = recs[min(start + lane, end - 1)];
 
-    // Load the region, dropping entries no request of this batch can see, and
-    // rebuild the open-addressing table in LDS (no tombstones ever reach HBM).
-    for (uint32_t s = t; s < R; s += kRegionThreads) {
+    Slot* tab = (Slot*)L.table + (size_t)(g - L.region_base) * S;
+    for (uint32_t s = lane; s < S; s += 64) s_occ[s] = 0;
+    wave_fence();
+    // Load the region, dropping entries no request of this batch can see, and rebuild
+    // the open-addressing table (no tombstones ever reach HBM).
+    for (uint32_t s = lane; s < S; s += 64) {
         const Slot v = tab[s];
         if (slot_live(L, v, batch_min)) {
-            uint32_t p = (uint32_t)v.tag & (R - 1);
-            while (atomicCAS(&s_occ[p], 0u, 1u) != 0u) p = (p + 1) & (R - 1);
+            uint32_t p = (uint32_t)v.tag & (S - 1);
+            while (atomicCAS(&s_occ[p], 0u, 1u) != 0u) p = (p + 1) & (S - 1);
             s_tag[p] = v.tag; s_a[p] = v.a; s_b[p] = v.b; s_c[p] = v.c;
         }
     }
-    __syncthreads();
+    wave_fence();
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0;
-    const Rec* recs = (const Rec*)a.rec;
-    const uint32_t end = start + cnt;
-    for (uint32_t gb = start; gb < end; gb += kRegionThreads) {
-        const uint32_t j = gb + t;
+    for (uint32_t gb = start; gb < end; gb += 64) {
+        const uint32_t j = gb + lane;
         const bool valid = j < end;
-        Req q{};
-        if (valid) q = Codec::dec(recs[j], base);
+        const Rec cur = nxt;
+        nxt = recs[min(gb + 64 + lane, end - 1)];   // unconditional: static vmcnt counting
+        const Req q = Codec::dec(cur, base);
         const bool live = valid && !q.invalid;
-        if (valid && q.invalid) {
-            a.res[j] = pack_result(false, kRemInvalid);
-            if (a.tok) a.tok[j] = __builtin_nan("");
-            ++n_invalid;
-        }
-        // ---- find or insert the key's slot
+        uint64_t out = pack_result(false, kRemInvalid);
+        double otok = __builtin_nan("");
+        n_invalid += (valid && q.invalid) ? 1u : 0u;
+        // ---- find or insert the key's slot (lookup phase, then claim phase)
         int32_t slot = -1;
         bool need = live, failed = false;
-        const uint32_t home = (uint32_t)q.h & (R - 1);
+        const uint32_t home = (uint32_t)q.h & (S - 1);
         for (;;) {
             uint32_t cand = kNone;
             if (need) {
                 uint32_t p = home;
-                for (uint32_t step = 0; step < R; ++step) {
+                for (uint32_t step = 0; step < S; ++step) {
                     if ((s_occ[p] & 1u) == 0u) { cand = p; break; }
                     if (s_tag[p] == q.h) { slot = (int32_t)p; need = false; break; }
-                    p = (p + 1) & (R - 1);
+                    p = (p + 1) & (S - 1);
                 }
                 if (need && cand == kNone) { need = false; failed = true; }
             }
-            __syncthreads();
+            wave_fence();
             if (need && atomicCAS(&s_occ[cand], 0u, 1u) == 0u) {
                 s_tag[cand] = q.h; s_a[cand] = 0; s_b[cand] = 0; s_c[cand] = 0;
                 slot = (int32_t)cand;
                 need = false;
             }
-            __syncthreads();
-            if (!__syncthreads_or(need)) break;
+            wave_fence();
+            if (!__any(need)) break;
         }
         if (failed) {
-            a.res[j] = pack_result(false, kRemError);
-            if (a.tok) a.tok[j] = __builtin_nan("");
+            out = pack_result(false, kRemError);
             ++n_caperr;
         }
         if (slot >= 0) atomicOr(&s_occ[slot], 2u);
         // ---- apply in arrival order: per round, the first state-changing request of
-        // each key applies; every earlier (non-mutating) request of that key is final.
+        // each key applies; the key's earlier (non-mutating) requests are final.
+        const uint64_t peers = wave_match((uint32_t)slot, kRegionBits, slot >= 0);
         bool pending = slot >= 0;
-        for (;;) {
-            Outcome o;
+        while (__any(pending)) {
+            Outcome o{};
             if (pending) {
                 o = tb ? tb_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot])
                        : sw_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot]);
-                if (o.mutate) atomicMin(&s_fm[slot], t);
             }
-            __syncthreads();
-            bool mine = false;
-            if (pending) {
-                const uint32_t fm = s_fm[slot];
-                if (t <= fm) {
-                    if (t == fm) {
-                        s_a[slot] = o.a; s_b[slot] = o.b; s_c[slot] = o.c;
-                        mine = true;
-                    }
-                    a.res[j] = pack_result(o.allowed, o.remaining);
-                    if (a.tok) a.tok[j] = o.tokens;
-                    n_allowed += o.allowed ? 1u : 0u;
-                    pending = false;
-                }
+            const uint64_t mut = __ballot(pending && o.mutate) & peers;
+            const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
+            if (pending && lane <= fm) {
+                if (lane == fm) { s_a[slot] = o.a; s_b[slot] = o.b; s_c[slot] = o.c; }
+                out = pack_result(o.allowed, o.remaining);
+                otok = o.tokens;
+                n_allowed += o.allowed ? 1u : 0u;
+                pending = false;
             }
-            __syncthreads();
-            if (mine) s_fm[slot] = kNone;
-            if (!__syncthreads_or(pending)) break;
+            wave_fence();
         }
+        const uint32_t w = valid ? j : pad;
+        res[w] = (Res)out;
+        if (TOK) a.tok[w] = otok;
     }
-    __syncthreads();
     // ---- write the region back (free slots as zeros)
     uint32_t touched = 0;
-    for (uint32_t s = t; s < R; s += kRegionThreads) {
+    for (uint32_t s = lane; s < S; s += 64) {
         const uint32_t o = s_occ[s];
         Slot v;
         if (o & 1u) { v.tag = s_tag[s]; v.a = s_a[s]; v.b = s_b[s]; v.c = s_c[s]; }
@@ -415,33 +449,55 @@ __global__ __launch_bounds__(kRegionThreads) void k_region(RegionArgs a) {
         tab[s] = v;
         touched += (o >> 1) & 1u;
     }
-    atomicAdd(&s_stat[0], n_allowed);
-    atomicAdd(&s_stat[1], n_invalid);
-    atomicAdd(&s_stat[2], n_caperr);
-    atomicAdd(&s_stat[3], touched);
-    __syncthreads();
-    if (t == 0) {
-        atomicAdd(&a.ctl->allowed, (unsigned long long)s_stat[0]);
-        atomicAdd(&a.ctl->invalid, (unsigned long long)s_stat[1]);
-        atomicAdd(&a.ctl->cap_err, (unsigned long long)s_stat[2]);
-        atomicAdd(&a.ctl->distinct, (unsigned long long)s_stat[3]);
+    for (int off = 32; off > 0; off >>= 1) {
+        n_allowed += __shfl_xor(n_allowed, off, 64);
+        n_invalid += __shfl_xor(n_invalid, off, 64);
+        n_caperr += __shfl_xor(n_caperr, off, 64);
+        touched += __shfl_xor(touched, off, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
+        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
+        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
+        atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
         atomicAdd(&a.ctl->regions, 1ULL);
     }
 }
 
 // ------------------------------------------------------------------ 5. unpermute
+template <class Res>
 __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
     const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
     const uint32_t t = threadIdx.x;
-    for (int r = 0; r < kTileItems; ++r) {
-        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
-        if (i >= a.n) break;
-        uint32_t p = a.pos0[i];
-        if (a.pos1) p = a.pos1[p];
-        const uint64_t v = a.res[p];
-        a.allowed[i] = (uint8_t)(v & 1u);
-        a.remaining[i] = (int64_t)v >> 1;
-        if (a.tokens_out) a.tokens_out[i] = a.tok ? a.tok[p] : __builtin_nan("");
+    const Res* __restrict__ res = (const Res*)a.res;
+    const uint32_t* __restrict__ pos0 = a.pos0;
+    const uint32_t* __restrict__ pos1 = a.pos1;
+    uint8_t* __restrict__ allowed = a.allowed;
+    int64_t* __restrict__ remaining = a.remaining;
+    constexpr int B = 8;                       // rounds whose loads are issued together
+    for (int r0 = 0; r0 < kTileItems; r0 += B) {
+        uint32_t p[B];
+        Res v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const uint32_t i = tile * (uint32_t)kTile + (uint32_t)(r0 + k) * kTileThreads + t;
+            p[k] = pos0[i < a.n ? i : 0];
+        }
+        if (pos1) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) p[k] = pos1[p[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const uint32_t i = tile * (uint32_t)kTile + (uint32_t)(r0 + k) * kTileThreads + t;
+            if (i < a.n) {
+                allowed[i] = (uint8_t)(v[k] & 1u);
+                remaining[i] = (int64_t)(v[k] >> 1) - kResBias;
+                if (a.tokens_out) a.tokens_out[i] = a.tok ? a.tok[p[k]] : __builtin_nan("");
+            }
+        }
     }
 }
 
@@ -602,14 +658,26 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
     return hipGetLastError();
 }
 
-hipError_t launch_region(const RegionArgs& a, bool wide, hipStream_t s) {
-    if (wide) hipLaunchKernelGGL((k_region<CodecW>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
-    else hipLaunchKernelGGL((k_region<CodecC>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
+template <class Codec, class Res>
+static void region_launch(const RegionArgs& a, hipStream_t s) {
+    if (a.tok) hipLaunchKernelGGL((k_region<Codec, Res, true>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
+    else hipLaunchKernelGGL((k_region<Codec, Res, false>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
+}
+
+hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
+    if (wide) region_launch<CodecW, uint64_t>(a, s);
+    else if (res_bytes == 1) region_launch<CodecC, uint8_t>(a, s);
+    else if (res_bytes == 2) region_launch<CodecC, uint16_t>(a, s);
+    else region_launch<CodecC, uint32_t>(a, s);
     return hipGetLastError();
 }
 
-hipError_t launch_unpermute(const UnpermArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_unpermute, dim3(a.n_tiles), dim3(kTileThreads), 0, s, a);
+hipError_t launch_unpermute(const UnpermArgs& a, int res_bytes, hipStream_t s) {
+    dim3 g(a.n_tiles), b(kTileThreads);
+    if (res_bytes == 8) hipLaunchKernelGGL(k_unpermute<uint64_t>, g, b, 0, s, a);
+    else if (res_bytes == 1) hipLaunchKernelGGL(k_unpermute<uint8_t>, g, b, 0, s, a);
+    else if (res_bytes == 2) hipLaunchKernelGGL(k_unpermute<uint16_t>, g, b, 0, s, a);
+    else hipLaunchKernelGGL(k_unpermute<uint32_t>, g, b, 0, s, a);
     return hipGetLastError();
 }
 

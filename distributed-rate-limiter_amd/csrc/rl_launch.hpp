@@ -51,16 +51,17 @@ struct RegionArgs {
     const uint32_t* rcount;    // [P]
     const uint8_t* region_lim; // [P]
     const DevLimiter* lims;
-    uint64_t* res;             // packed results in region order
+    void* res;                 // packed results in region order (u32 compact, u64 wide)
     double* tok;               // nullable: TB fp64 balances in region order
     BatchCtl* ctl;
     uint32_t n_regions;
+    uint32_t n_total;          // batch size: res/tok carry 64 padding entries past it
 };
 
 struct UnpermArgs {
     const uint32_t* pos0;
     const uint32_t* pos1;      // nullable
-    const uint64_t* res;
+    const void* res;
     const double* tok;         // nullable
     uint8_t* allowed;
     int64_t* remaining;
@@ -95,8 +96,8 @@ hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, ui
 hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hipStream_t s);
 hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
                            uint32_t cols, hipStream_t s);
-hipError_t launch_region(const RegionArgs& a, bool wide, hipStream_t s);
-hipError_t launch_unpermute(const UnpermArgs& a, hipStream_t s);
+hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
+hipError_t launch_unpermute(const UnpermArgs& a, int res_bytes, hipStream_t s);
 hipError_t launch_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n,
                                hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);

@@ -30,6 +30,7 @@ SW, TB = 0, 1
 OP_ACQUIRE, OP_PEEK, OP_RESET = 0, 1, 2
 REM_UNKNOWN, REM_INVALID, REM_ERROR = -1, -2, -3
 OPT_STAGE_TIMING = 1
+REGION_SLOTS = 256          # kRegionSlots in csrc/rl_device.hpp (state slots per region)
 DIST_UNIFORM, DIST_ZIPF = 0, 1
 
 EXPORTS = [

@@ -134,12 +134,14 @@ def test_state_persists_across_many_small_batches():
 
 
 def test_ttl_reclamation_reuses_slots():
-    # tiny table (1 region = 512 slots): 3 waves of 300 distinct keys each, 10 s apart with
-    # a 1 s window -> earlier keys expire and their slots must be reclaimed.
+    # tiny table (1 region = REGION_SLOTS slots): 3 waves of 0.6*slots distinct keys each,
+    # 10 s apart with a 1 s window -> earlier keys expire and their slots must be reclaimed
+    # (two waves together would not fit).
     lims = [[rl_amd.TB, 5, 1000, 2.0, 1], [rl_amd.SW, 5, 1000, 0.0, 1]]
     parts = []
+    nk = int(rl_amd.REGION_SLOTS * 0.6)
     for w in range(3):
-        k = rl_amd.mix64(np.arange(300, dtype=np.uint64) + np.uint64(w * 1000))
+        k = rl_amd.mix64(np.arange(nk, dtype=np.uint64) + np.uint64(w * 1000))
         k = np.repeat(k, 3)
         now = np.full(k.shape, (T0 + w * 10_000) * NS, np.int64) + np.arange(k.size) * 1000
         parts.append((k, np.ones(k.size, np.int32), now, (np.arange(k.size) % 2).astype(np.uint16)))
@@ -156,12 +158,12 @@ def test_ttl_reclamation_reuses_slots():
 
 def test_capacity_overflow_reported():
     e = rl_amd.Engine(max_batch=1 << 16, capacity=1)
-    e.add_limiter(rl_amd.TB, 5, 60000, 1.0, capacity=1)     # one region of 512 slots
+    e.add_limiter(rl_amd.TB, 5, 60000, 1.0, capacity=1)     # one region of REGION_SLOTS slots
     keys = rl_amd.mix64(np.arange(2000, dtype=np.uint64))
     a, r, t, st = e.execute(keys, np.ones(2000, np.int32), np.full(2000, T0 * NS, np.int64))
     assert st == rl_amd.RL_E_CAPACITY
-    assert (r == rl_amd.REM_ERROR).sum() == 2000 - 512
-    assert a.sum() == 512
+    assert (r == rl_amd.REM_ERROR).sum() == 2000 - rl_amd.REGION_SLOTS
+    assert a.sum() == rl_amd.REGION_SLOTS
 
 
 def test_wide_records_large_max():
