@@ -27,18 +27,27 @@ constexpr int64_t kRemError = -3;     // state-table region full
 
 // State table: a limiter's keys live in 2^k regions of kRegionSlots slots. One
 // wavefront owns a region for a whole batch (its 8 KB image lives in that wave's
-// LDS), so a region needs no atomics in HBM and no workgroup barriers.
+// LDS), so a region needs no atomics in HBM. The batch is partitioned by BIN =
+// kRegionsPerBin consecutive regions; one 8-wave workgroup owns a bin and each wave
+// picks its region's requests out of the bin's arrival-ordered stream in LDS. Fewer,
+// larger bins keep the partition's open write lines (bins x tiles in flight x 128 B)
+// inside each XCD's 4 MB L2.
 constexpr int kRegionSlots = 256;                 // slots per region (load <= ~0.5)
 constexpr int kRegionBits = 8;
-constexpr int kRegionThreads = 64;                // one wave per region
+constexpr int kRegionsPerBin = 8;                 // = waves per bin workgroup
+constexpr int kBinShift = 3;
+constexpr int kBinThreads = 64 * kRegionsPerBin;  // 512
+constexpr int kChunk = kBinThreads;               // records staged per step
+constexpr int kRing = 128;                        // per-wave pending ring (< 64 + 64 entries)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // Partition tiles (upsweep / scatter / unpermute all share this tiling). 64K
-// requests per tile: with <= 8192 bins a tile writes >= 8 records (128 B) per bin.
+// requests per tile; grids are persistent (one workgroup per CU) and walk the tiles
+// so that the 32 workgroups of an XCD work on 32 consecutive tiles at a time.
 constexpr int kTileThreads = 256;
 constexpr int kTileItems = 256;
 constexpr int kTile = kTileThreads * kTileItems;  // 65536 requests per tile
-constexpr int kMaxDigitBits = 13;                 // <= 8192 bins per pass
+constexpr int kMaxDigitBits = 10;                 // <= 1024 bins per pass
 
 // Compact record field limits.
 constexpr uint32_t kPermitBits = 22;

@@ -29,7 +29,7 @@ const char* kStageNames[kStages] = {"upsweep0", "scan0", "scatter0", "upsweep1",
                                     "scatter1", "region_offsets", "region", "unpermute", "total"};
 const int kStagePairs[kStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6},
                                      {6, 7}, {7, 8}, {8, 9}, {0, 9}};
-constexpr int kRing = 64;
+constexpr int kEvRing = 64;
 
 struct HostLimiter {
     rl_limiter_config cfg;
@@ -96,7 +96,7 @@ struct rl_engine {
     size_t route_cap = 0;
     uint32_t* route_counts = nullptr;
 
-    hipEvent_t ev[kRing][kMarks] = {};
+    hipEvent_t ev[kEvRing][kMarks] = {};
     int ring_used = 0;                      // batches recorded since the last query
     int ring_next = 0;
     bool timing = false;
@@ -104,6 +104,7 @@ struct rl_engine {
     bool pending_status = false;
     int last_status = RL_OK;
     uint64_t last_n = 0;
+    uint32_t ablate = 0;                    // rl_tune("ablate"), measurement only
 };
 
 #define HIP_OK(x)                                                      \
@@ -187,7 +188,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     }
     e->timing = (o.flags & RL_OPT_STAGE_TIMING) != 0;
     if (e->timing)
-        for (int r = 0; r < kRing; ++r)
+        for (int r = 0; r < kEvRing; ++r)
             for (int i = 0; i < kMarks; ++i) (void)hipEventCreate(&e->ev[r][i]);
     int rc = dalloc(&e->d_ctl, 1);
     if (rc == RL_OK && hipHostMalloc((void**)&e->h_ctl, sizeof(BatchCtl)) != hipSuccess) rc = RL_E_NOMEM;
@@ -213,7 +214,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
     dfree(e->route_scratch); dfree(e->route_counts);
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
-    for (int r = 0; r < kRing; ++r)
+    for (int r = 0; r < kEvRing; ++r)
         for (int i = 0; i < kMarks; ++i) if (e->ev[r][i]) (void)hipEventDestroy(e->ev[r][i]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -256,7 +257,7 @@ extern "C" int rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* c, uint1
     uint64_t per_shard = (cap + e->opts.shard_count - 1) / e->opts.shard_count;
     uint64_t slots = std::max<uint64_t>(per_shard * 2, kRegionSlots);   // load <= 0.5
     uint64_t regions = (slots + kRegionSlots - 1) / kRegionSlots;
-    int k = ceil_log2(regions);
+    int k = std::max(ceil_log2(regions), kBinShift);     // whole bins of kRegionsPerBin regions
     if (k + e->shard_bits > 40) return RL_E_INVALID_ARG;
     if ((uint64_t)e->n_regions + (1ULL << k) > (1ULL << 24)) return RL_E_LIMITERS;
     DevLimiter& d = h.dev;
@@ -360,7 +361,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     const int res_bytes = res_bytes_for(max_any, wide);
     const uint32_t nt = (uint32_t)((n + kTile - 1) / kTile);
-    const int bitsP = std::max(1, ceil_log2(e->n_regions));
+    const uint32_t n_bins = e->n_regions / kRegionsPerBin;
+    const int bitsP = std::max(1, ceil_log2(n_bins));
     const int passes = bitsP <= kMaxDigitBits ? 1 : 2;
     if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
     const int d0 = passes == 1 ? bitsP : bitsP - bitsP / 2;
@@ -368,7 +370,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     int rc = ensure_scratch(e, n, wide, 1u << std::max(d0, d1), nt);
     if (rc != RL_OK) return rc;
     const uint32_t cols = 4096;
-    const size_t padded = ((size_t)e->n_regions + cols - 1) / cols * cols;
+    const size_t padded = ((size_t)n_bins + cols - 1) / cols * cols;
     if (passes == 2) {
         rc = ensure_regions(e, padded);
         if (rc != RL_OK) return rc;
@@ -380,7 +382,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.key = key; pa.permits = permits; pa.now_ns = now_ns; pa.limiter = limiter; pa.op = op;
     pa.n = (uint32_t)n; pa.n_tiles = nt; pa.n_lim = (uint32_t)e->lims.size();
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = e->d_ctl;
-    pa.counts = e->counts; pa.bin_base = e->bin_base;
+    pa.counts = e->counts; pa.bin_base = e->bin_base; pa.ablate = e->ablate;
     // ---- pass 0 (low digit) from the caller's arrays
     pa.digit_shift = 0; pa.digit_bits = d0;
     pa.region_count = nullptr;
@@ -429,19 +431,20 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     RegionArgs ra{};
     ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.region_lim = e->d_region_lim;
     ra.lims = e->d_lims; ra.res = e->res; ra.tok = tokens_after ? e->tok : nullptr;
-    ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n;
+    ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
+    ra.shard_bits = e->shard_bits;
     HIP_OK(launch_region(ra, wide, res_bytes, s));
     mark(e, 8);
     UnpermArgs ua{};
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
     ua.tok = tokens_after ? e->tok : nullptr;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
-    ua.n = (uint32_t)n; ua.n_tiles = nt;
+    ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate;
     HIP_OK(launch_unpermute(ua, res_bytes, s));
     mark(e, 9);
     if (e->timing) {
-        e->ring_next = (e->ring_next + 1) % kRing;
-        e->ring_used = std::min(e->ring_used + 1, kRing);
+        e->ring_next = (e->ring_next + 1) % kEvRing;
+        e->ring_used = std::min(e->ring_used + 1, kEvRing);
     }
     HIP_OK(hipMemcpyAsync(e->h_ctl, e->d_ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, s));
     e->pending_status = true;
@@ -598,7 +601,7 @@ extern "C" int rl_stage_times(rl_engine* e, const char** names, float* ms, int c
     for (int i = 0; i < k; ++i) {
         double acc = 0.0;
         for (int b = 0; b < nb; ++b) {
-            const int r = (e->ring_next - 1 - b + kRing) % kRing;
+            const int r = (e->ring_next - 1 - b + kEvRing) % kEvRing;
             float x = 0.f;
             if (hipEventElapsedTime(&x, e->ev[r][kStagePairs[i][0]], e->ev[r][kStagePairs[i][1]]) != hipSuccess)
                 x = 0.f;
@@ -609,6 +612,13 @@ extern "C" int rl_stage_times(rl_engine* e, const char** names, float* ms, int c
     }
     e->ring_used = 0;
     return k;
+}
+
+extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
+    if (!e || !key) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (std::strcmp(key, "ablate") == 0) { e->ablate = (uint32_t)value; return RL_OK; }
+    return RL_E_INVALID_ARG;
 }
 
 extern "C" int rl_sync(rl_engine* e) {

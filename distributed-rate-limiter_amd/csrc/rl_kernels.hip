@@ -4,21 +4,25 @@
 // the other requests of its (limiter, key) WITHOUT a full sort:
 //
 //   1. k_upsweep  : per 64K-request tile, histogram of the partition digit of each
-//                   request's state-table REGION (region = top bits of mix64(key)).
+//                   request's BIN (bin = 8 consecutive state-table regions; region =
+//                   top bits of mix64(key)).
 //   2. k_scan_rows/k_scan_small : exclusive scan of the [bin][tile] histogram.
 //   3. k_scatter  : stable partition (wave ballot-match ranking) of the requests
-//                   into region order, packed into 16-byte records.
-//   (1-3 repeat once more when a limiter set has > 8192 regions.)
-//   4. k_region   : one WAVE per region. Loads the region's 256 state slots (8 KB)
-//                   into LDS once, streams the region's records in arrival order 64
-//                   at a time, applies the reference semantics per key in order (deny
-//                   never mutates, so a group needs 1 + (#state changes of its busiest
-//                   key) rounds), writes the region back once.
+//                   into bin order, packed into 16-byte records.
+//   (1-3 repeat once more when a limiter set has > 1024 bins.)
+//   4. k_bin      : one 8-wave workgroup per bin, one WAVE per region. Each wave loads
+//                   its region's 256 state slots (8 KB) into LDS once; the bin's
+//                   records are staged through LDS 512 at a time in arrival order,
+//                   every wave compacts its own region's requests into a ring and
+//                   applies the reference semantics per key in order (deny never
+//                   mutates, so a 64-request group needs 1 + (#state changes of its
+//                   busiest key) rounds); the regions are written back once.
 //   5. k_unpermute: results back to the caller's order (allowed u8, remaining i64).
 //
-// Tiles are mapped XCD-aware (consecutive tiles on one XCD) so the per-tile
-// histogram columns, the record runs of one bin and the result gathers of
-// neighbouring tiles combine in that XCD's L2 instead of going to HBM as partial lines.
+// Partition and unpermute grids are persistent and walk tiles XCD-aware: at any
+// time the 32 CUs of an XCD work on 32 consecutive tiles, so the per-bin record runs
+// they write (and the result runs they gather) share lines in that XCD's L2.
+#include <algorithm>
 #include <type_traits>
 
 #include "rl_launch.hpp"
@@ -89,9 +93,15 @@ __device__ inline void load_lim_lds(LimLds& L, const PartArgs& a) {
     }
 }
 
-// Global region id of element i (pass 0: raw arrays; later passes: records).
+// Tile processed by this workgroup at iteration `it` of a persistent grid: the
+// workgroups of one XCD (blocks b, b+8, ...) take consecutive tiles.
+__device__ inline uint32_t tile_at(uint32_t it) {
+    return it * gridDim.x + xcd_remap(blockIdx.x, gridDim.x);
+}
+
+// Global bin id of element i (pass 0: raw arrays; later passes: records).
 template <class Codec, bool RAW>
-__device__ inline uint32_t region_of(const PartArgs& a, uint32_t i, const LimLds& L) {
+__device__ inline uint32_t bin_of(const PartArgs& a, uint32_t i, const LimLds& L) {
     uint64_t h;
     uint32_t lim;
     if constexpr (RAW) {
@@ -103,7 +113,7 @@ __device__ inline uint32_t region_of(const PartArgs& a, uint32_t i, const LimLds
         h = r->h;
         lim = Codec::limiter_of(*r);
     }
-    return L.base[lim] + region_local(h, a.shard_bits, L.bits[lim]);
+    return (L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> kBinShift;
 }
 
 // ------------------------------------------------------------------ 1. upsweep
@@ -113,7 +123,6 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
     __shared__ LimLds L;
     const uint32_t t = threadIdx.x;
     const uint32_t bins = 1u << a.digit_bits;
-    for (uint32_t b = t; b < bins; b += kTileThreads) hist[b] = 0;
     load_lim_lds(L, a);
     if constexpr (RAW) {
         if (blockIdx.x == 0 && t == 0) {
@@ -125,21 +134,25 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
             c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = 0;
         }
     }
-    __syncthreads();
-    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
     const uint32_t mask = bins - 1;
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t tile = tile_at(it);
+        if (tile >= a.n_tiles) break;
+        for (uint32_t b = t; b < bins; b += kTileThreads) hist[b] = 0;
+        __syncthreads();
 #pragma unroll 8
-    for (int r = 0; r < kTileItems; ++r) {
-        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
-        if (i < a.n) {
-            const uint32_t g = region_of<Codec, RAW>(a, i, L);
-            atomicAdd(&hist[(g >> a.digit_shift) & mask], 1u);
-            if (a.region_count) atomicAdd(&a.region_count[g], 1u);
+        for (int r = 0; r < kTileItems; ++r) {
+            const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+            if (i < a.n) {
+                const uint32_t g = bin_of<Codec, RAW>(a, i, L);
+                atomicAdd(&hist[(g >> a.digit_shift) & mask], 1u);
+                if (a.region_count) atomicAdd(&a.region_count[g], 1u);
+            }
         }
+        __syncthreads();
+        for (uint32_t b = t; b < bins; b += kTileThreads)
+            a.counts[(size_t)b * a.n_tiles + tile] = hist[b];
     }
-    __syncthreads();
-    for (uint32_t b = t; b < bins; b += kTileThreads)
-        a.counts[(size_t)b * a.n_tiles + tile] = hist[b];
 }
 
 // ------------------------------------------------------------------ 2. scans
@@ -226,85 +239,95 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     __shared__ uint64_t s_mm[2][kTileThreads / 64];
     const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t bins = 1u << a.digit_bits, mask = bins - 1;
-    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
-    const uint32_t tile0 = tile * (uint32_t)kTile;
-    for (uint32_t b = t; b < bins; b += kTileThreads) {
-        cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
-#pragma unroll
-        for (int w = 0; w < kTileThreads / 64; ++w) cntw[w][b] = 0;
-    }
     load_lim_lds(L, a);
     int64_t base = 0;
     if constexpr (RAW) base = a.ctl->base_ms;
-    // two rounds of inputs in flight; out-of-range lanes re-load element n-1 so every
-    // wave issues the same loads and stores each round (static vmcnt counting: the
-    // waits for round r+2's inputs never include round r's scattered stores).
     const uint32_t last = a.n - 1;
-    ScatterIn<Codec, RAW> nx1, nx2;
-    nx1.load(a, min(tile0 + t, last));
-    nx2.load(a, min(tile0 + kTileThreads + t, last));
-    __syncthreads();
     uint64_t mn = ~0ULL, mx = 0;
     bool overflow = false;
-    for (int r = 0; r < kTileItems; ++r) {
-        const uint32_t i = tile0 + (uint32_t)r * kTileThreads + t;
-        const bool active = i < a.n;
-        const ScatterIn<Codec, RAW> in = nx1;
-        nx1 = nx2;
-        nx2.load(a, min(i + 2 * kTileThreads, last));
-        Rec rec{};
-        uint32_t d = 0;
-        if (active) {
-            if constexpr (RAW) {
-                uint32_t lim = in.lim, op = in.op;
-                const int32_t p = in.permits;
-                const int64_t now_ms = floor_div_ms(in.now_ns);
-                const bool lim_ok = lim < a.n_lim;
-                if (!lim_ok) lim = 0;
-                const bool invalid = !lim_ok || op > 2u || (op == 0u && p <= 0);
-                if (op > 2u) op = 0;
-                const uint64_t h = mix64(in.key);
-                rec = Codec::enc(h, now_ms, base, p, op, lim, invalid);
-                const int64_t rel = now_ms - base;
-                overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
-                const uint64_t k = ord_key(now_ms);
-                mn = k < mn ? k : mn;
-                mx = k > mx ? k : mx;
-                d = ((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.digit_shift) & mask;
-            } else {
-                rec = in.rec;
-                const uint32_t lim = Codec::limiter_of(rec);
-                d = ((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.digit_shift) & mask;
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t tile = tile_at(it);
+        if (tile >= a.n_tiles) break;
+        const uint32_t tile0 = tile * (uint32_t)kTile;
+        __syncthreads();     // previous tile's LDS users are done
+        for (uint32_t b = t; b < bins; b += kTileThreads) {
+            cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
+#pragma unroll
+            for (int w = 0; w < kTileThreads / 64; ++w) cntw[w][b] = 0;
+        }
+        // two rounds of inputs in flight; out-of-range lanes re-load element n-1 so every
+        // wave issues the same loads and stores each round (static vmcnt counting: the
+        // waits for round r+2's inputs never include round r's scattered stores).
+        ScatterIn<Codec, RAW> nx1, nx2;
+        nx1.load(a, min(tile0 + t, last));
+        nx2.load(a, min(tile0 + kTileThreads + t, last));
+        __syncthreads();
+        for (int r = 0; r < kTileItems; ++r) {
+            const uint32_t i = tile0 + (uint32_t)r * kTileThreads + t;
+            const bool active = i < a.n;
+            const ScatterIn<Codec, RAW> in = nx1;
+            nx1 = nx2;
+            nx2.load(a, min(i + 2 * kTileThreads, last));
+            Rec rec{};
+            uint32_t d = 0;
+            if (active) {
+                if constexpr (RAW) {
+                    uint32_t lim = in.lim, op = in.op;
+                    const int32_t p = in.permits;
+                    const int64_t now_ms = floor_div_ms(in.now_ns);
+                    const bool lim_ok = lim < a.n_lim;
+                    if (!lim_ok) lim = 0;
+                    const bool invalid = !lim_ok || op > 2u || (op == 0u && p <= 0);
+                    if (op > 2u) op = 0;
+                    const uint64_t h = mix64(in.key);
+                    rec = Codec::enc(h, now_ms, base, p, op, lim, invalid);
+                    const int64_t rel = now_ms - base;
+                    overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
+                    const uint64_t k = ord_key(now_ms);
+                    mn = k < mn ? k : mn;
+                    mx = k > mx ? k : mx;
+                    d = (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> kBinShift)
+                         >> a.digit_shift) & mask;
+                } else {
+                    rec = in.rec;
+                    const uint32_t lim = Codec::limiter_of(rec);
+                    d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> kBinShift)
+                         >> a.digit_shift) & mask;
+                }
             }
+            const uint32_t abl = a.ablate;
+            const uint64_t m = (abl & kAblNoMatch) ? (1ULL << lane) : wave_match(d, a.digit_bits, active);
+            const uint32_t lr = popc_below(m);
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            const bool leader = active && lr == 0;
+            if (leader) cntw[wid][d] = (uint8_t)cnt;
+            if (!(abl & kAblNoBarrier)) __syncthreads();
+            uint32_t pos = 0;
+            if (active) {
+                pos = cur[d] + lr;
+                for (uint32_t w = 0; w < wid; ++w) pos += cntw[w][d];
+            }
+            if (!(abl & kAblNoBarrier)) __syncthreads();
+            if (leader) {
+                atomicAdd(&cur[d], cnt);
+                cntw[wid][d] = 0;
+            }
+            if (abl & (kAblNoMatch | kAblNoBarrier)) pos = min(pos, a.n - 1);
+            // inactive lanes write to the padding slot past n (buffers carry spare entries)
+            uint32_t wpos = active ? pos : a.n + t;
+            if (abl & kAblSeqRecStore) wpos = active ? i : a.n + t;
+            if (!(abl & kAblNoRecStore)) ((Rec*)a.rec_out)[wpos] = rec;
+            if (!(abl & kAblNoPosStore)) a.pos_out[active ? i : a.n + t] = pos;
         }
-        const uint64_t m = wave_match(d, a.digit_bits, active);
-        const uint32_t lr = popc_below(m);
-        const uint32_t cnt = (uint32_t)__popcll(m);
-        const bool leader = active && lr == 0;
-        if (leader) cntw[wid][d] = (uint8_t)cnt;
-        __syncthreads();
-        uint32_t pos = 0;
-        if (active) {
-            pos = cur[d] + lr;
-            for (uint32_t w = 0; w < wid; ++w) pos += cntw[w][d];
-        }
-        __syncthreads();
-        if (leader) {
-            atomicAdd(&cur[d], cnt);
-            cntw[wid][d] = 0;
-        }
-        // inactive lanes write to the padding slot past n (buffers carry 256 spare entries)
-        const uint32_t wpos = active ? pos : a.n + t;
-        ((Rec*)a.rec_out)[wpos] = rec;
-        a.pos_out[active ? i : a.n + t] = pos;
     }
     if constexpr (RAW) {
-        // min / max now over the tile -> one atomic each
+        // min / max now over this workgroup's tiles -> one atomic each
         for (int o = 32; o > 0; o >>= 1) {
             const uint64_t a1 = __shfl_xor(mn, o, 64), b1 = __shfl_xor(mx, o, 64);
             mn = a1 < mn ? a1 : mn;
             mx = b1 > mx ? b1 : mx;
         }
+        __syncthreads();
         if (lane == 0) { s_mm[0][wid] = mn; s_mm[1][wid] = mx; }
         const bool any_over = __syncthreads_or(overflow);
         if (t == 0) {
@@ -312,139 +335,211 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                 mn = s_mm[0][w] < mn ? s_mm[0][w] : mn;
                 mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
             }
-            atomicMin((unsigned long long*)&a.ctl->min_now_key, (unsigned long long)mn);
-            atomicMax((unsigned long long*)&a.ctl->max_now_key, (unsigned long long)mx);
+            if (mn != ~0ULL) atomicMin((unsigned long long*)&a.ctl->min_now_key, (unsigned long long)mn);
+            if (mx != 0) atomicMax((unsigned long long*)&a.ctl->max_now_key, (unsigned long long)mx);
             if (any_over) atomicOr(&a.ctl->span_overflow, 1u);
         }
     }
 }
 
-// ------------------------------------------------------------------ 4. region
-// One wavefront per region. The region's 256 slots (8 KB) are loaded into this
-// wave's LDS once, rebuilt without expired entries, the region's records are streamed
-// in arrival order 64 at a time, and the image is written back once. Everything is
-// wave-synchronous: no workgroup barriers, no HBM atomics.
+// ------------------------------------------------------------------ 4. bin / region
 __device__ inline void wave_fence() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }
 
-template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(kRegionThreads) void k_region(RegionArgs a) {
+template <class Codec>
+struct BinLds {
     using Rec = typename Codec::Rec;
-    constexpr uint32_t S = kRegionSlots;
-    __shared__ uint64_t s_tag[S], s_a[S], s_b[S], s_c[S];
-    __shared__ uint32_t s_occ[S];   // bit0 occupied, bit1 touched by this batch
+    uint64_t tag[kRegionsPerBin][kRegionSlots];
+    uint64_t sa[kRegionsPerBin][kRegionSlots];
+    uint64_t sb[kRegionsPerBin][kRegionSlots];
+    uint64_t sc[kRegionsPerBin][kRegionSlots];
+    uint32_t occ[kRegionsPerBin][kRegionSlots];   // bit0 occupied, bit1 touched by this batch
+    Rec stage[kChunk];                            // the bin's next records, arrival order
+    Rec ring[kRegionsPerBin][kRing];              // per-wave pending requests
+    uint32_t ring_pos[kRegionsPerBin][kRing];     // ... and their positions (result index)
+    uint32_t stat[4];
+};
 
-    const uint32_t g = blockIdx.x;
-    const uint32_t cnt = a.rcount[g];
-    if (cnt == 0) return;
-    const uint32_t start = a.rstart[g];
-    const uint32_t end = start + cnt;
-    const uint32_t lane = threadIdx.x;
-    const DevLimiter L = a.lims[a.region_lim[g]];
+// One wave applies up to 64 of its region's pending requests (ring[head..head+n)) in
+// arrival order against its LDS region image.
+template <class Codec, class Res, bool TOK>
+__device__ inline void wave_apply(const RegionArgs& a, BinLds<Codec>& S, const DevLimiter& L,
+                                  uint32_t w, uint32_t lane, uint32_t head, uint32_t n,
+                                  int64_t base, uint32_t pad, uint32_t& n_allowed,
+                                  uint32_t& n_invalid, uint32_t& n_caperr) {
+    using Rec = typename Codec::Rec;
+    constexpr uint32_t NS = kRegionSlots;
+    uint64_t* s_tag = S.tag[w];
+    uint64_t* s_a = S.sa[w];
+    uint64_t* s_b = S.sb[w];
+    uint64_t* s_c = S.sc[w];
+    uint32_t* s_occ = S.occ[w];
     const bool tb = L.algo == kAlgoTB;
+    const bool valid = lane < n;
+    const uint32_t ri = (head + (valid ? lane : 0u)) % kRing;
+    const Rec cur = S.ring[w][ri];
+    const uint32_t j = valid ? S.ring_pos[w][ri] : pad;
+    const Req q = Codec::dec(cur, base);
+    const bool live = valid && !q.invalid;
+    uint64_t out = pack_result(false, kRemInvalid);
+    double otok = __builtin_nan("");
+    n_invalid += (valid && q.invalid) ? 1u : 0u;
+    // ---- find or insert the key's slot (lookup phase, then claim phase)
+    int32_t slot = -1;
+    bool need = live, failed = false;
+    const uint32_t home = (uint32_t)q.h & (NS - 1);
+    if (a.ablate & kAblNoProbe) { if (need) slot = (int32_t)home; need = false; }
+    for (;;) {
+        if (!__any(need)) break;
+        uint32_t cand = kNone;
+        if (need) {
+            uint32_t p = home;
+            for (uint32_t step = 0; step < NS; ++step) {
+                const uint32_t o = s_occ[p];
+                const uint64_t tg = s_tag[p];
+                if ((o & 1u) == 0u) { cand = p; break; }
+                if (tg == q.h) { slot = (int32_t)p; need = false; break; }
+                p = (p + 1) & (NS - 1);
+            }
+            if (need && cand == kNone) { need = false; failed = true; }
+        }
+        wave_fence();
+        if (need && atomicCAS(&s_occ[cand], 0u, 1u) == 0u) {
+            s_tag[cand] = q.h; s_a[cand] = 0; s_b[cand] = 0; s_c[cand] = 0;
+            slot = (int32_t)cand;
+            need = false;
+        }
+        wave_fence();
+    }
+    if (failed) {
+        out = pack_result(false, kRemError);
+        ++n_caperr;
+    }
+    if (slot >= 0) atomicOr(&s_occ[slot], 2u);
+    // ---- apply in arrival order: per round, the first state-changing request of each
+    // key applies; the key's earlier (non-mutating) requests are final.
+    const bool one_round = (a.ablate & kAblNoRounds) != 0;
+    const uint64_t peers = one_round ? (1ULL << lane)
+                                     : wave_match((uint32_t)slot, kRegionBits, slot >= 0);
+    bool pending = slot >= 0;
+    while (__any(pending)) {
+        Outcome o{};
+        if (pending) {
+            if (a.ablate & kAblNoStep) {
+                o.mutate = (q.permits & 1) != 0; o.allowed = o.mutate; o.remaining = q.permits;
+                o.a = s_a[slot]; o.b = s_b[slot]; o.c = s_c[slot];
+            } else {
+                o = tb ? tb_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot])
+                       : sw_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot]);
+            }
+        }
+        const uint64_t mut = __ballot(pending && o.mutate) & peers;
+        const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
+        if (pending && lane <= fm) {
+            if (lane == fm) { s_a[slot] = o.a; s_b[slot] = o.b; s_c[slot] = o.c; }
+            out = pack_result(o.allowed, o.remaining);
+            otok = o.tokens;
+            n_allowed += o.allowed ? 1u : 0u;
+            pending = false;
+        }
+        wave_fence();
+    }
+    ((Res*)a.res)[j] = (Res)out;
+    if (TOK) a.tok[j] = otok;
+}
+
+template <class Codec, class Res, bool TOK>
+__global__ __launch_bounds__(kBinThreads) void k_bin(RegionArgs a) {
+    using Rec = typename Codec::Rec;
+    constexpr uint32_t NS = kRegionSlots;
+    __shared__ BinLds<Codec> S;
+
+    const uint32_t bin = blockIdx.x;
+    const uint32_t cnt = a.rcount[bin];
+    if (cnt == 0) return;
+    const uint32_t start = a.rstart[bin];
+    const uint32_t end = start + cnt;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t region = bin * kRegionsPerBin + w;
+    const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
     const int64_t batch_min = (int64_t)(a.ctl->min_now_key ^ 0x8000000000000000ULL);
-    Res* res = (Res*)a.res;
+    const uint32_t pad = a.n_total + lane;          // padding slot for idle lanes
     const Rec* recs = (const Rec*)a.rec;
-    const uint32_t pad = a.n_total + lane;       // padding slot for lanes past `end`
 
     if (a.ctl->span_overflow != 0) {
         // compact records cannot represent this batch's time span: reject it whole,
         // before any state is touched (the host reports RL_E_INVALID_ARG).
-        for (uint32_t j = start + lane; j < end; j += 64) {
-            res[j] = (Res)pack_result(false, kRemInvalid);
+        for (uint32_t j = start + t; j < end; j += kBinThreads) {
+            ((Res*)a.res)[j] = (Res)pack_result(false, kRemInvalid);
             if (TOK) a.tok[j] = __builtin_nan("");
         }
         return;
     }
-    // prefetch the first group of records while the region image loads
-    Rec nxt = recs[min(start + lane, end - 1)];
+    Rec nxt = recs[min(start + t, end - 1)];        // first chunk, in flight during the load
 
-    Slot* tab = (Slot*)L.table + (size_t)(g - L.region_base) * S;
-    for (uint32_t s = lane; s < S; s += 64) s_occ[s] = 0;
+    // ---- load this wave's region, dropping entries no request of this batch can see,
+    // and rebuild its open-addressing table (no tombstones ever reach HBM)
+    Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
+    for (uint32_t s = lane; s < NS; s += 64) S.occ[w][s] = 0;
+    if (t < 4) S.stat[t] = 0;
     wave_fence();
-    // Load the region, dropping entries no request of this batch can see, and rebuild
-    // the open-addressing table (no tombstones ever reach HBM).
-    for (uint32_t s = lane; s < S; s += 64) {
+    for (uint32_t s = lane; s < NS; s += 64) {
         const Slot v = tab[s];
         if (slot_live(L, v, batch_min)) {
-            uint32_t p = (uint32_t)v.tag & (S - 1);
-            while (atomicCAS(&s_occ[p], 0u, 1u) != 0u) p = (p + 1) & (S - 1);
-            s_tag[p] = v.tag; s_a[p] = v.a; s_b[p] = v.b; s_c[p] = v.c;
+            uint32_t p = (uint32_t)v.tag & (NS - 1);
+            while (atomicCAS(&S.occ[w][p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+            S.tag[w][p] = v.tag; S.sa[w][p] = v.a; S.sb[w][p] = v.b; S.sc[w][p] = v.c;
         }
     }
     wave_fence();
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0;
-    for (uint32_t gb = start; gb < end; gb += 64) {
-        const uint32_t j = gb + lane;
-        const bool valid = j < end;
-        const Rec cur = nxt;
-        nxt = recs[min(gb + 64 + lane, end - 1)];   // unconditional: static vmcnt counting
-        const Req q = Codec::dec(cur, base);
-        const bool live = valid && !q.invalid;
-        uint64_t out = pack_result(false, kRemInvalid);
-        double otok = __builtin_nan("");
-        n_invalid += (valid && q.invalid) ? 1u : 0u;
-        // ---- find or insert the key's slot (lookup phase, then claim phase)
-        int32_t slot = -1;
-        bool need = live, failed = false;
-        const uint32_t home = (uint32_t)q.h & (S - 1);
-        for (;;) {
-            uint32_t cand = kNone;
-            if (need) {
-                uint32_t p = home;
-                for (uint32_t step = 0; step < S; ++step) {
-                    if ((s_occ[p] & 1u) == 0u) { cand = p; break; }
-                    if (s_tag[p] == q.h) { slot = (int32_t)p; need = false; break; }
-                    p = (p + 1) & (S - 1);
-                }
-                if (need && cand == kNone) { need = false; failed = true; }
+    uint32_t head = 0, count = 0;                    // this wave's ring (wave-uniform)
+    for (uint32_t c0 = start; c0 < end; c0 += kChunk) {
+        const uint32_t m = min((uint32_t)kChunk, end - c0);
+        __syncthreads();                             // every wave is done with `stage`
+        S.stage[t] = nxt;
+        nxt = recs[min(c0 + kChunk + t, end - 1)];
+        __syncthreads();
+        // each wave takes its region's requests out of the chunk, in arrival order, and
+        // applies them 64 at a time
+        for (uint32_t sl = 0; sl < (uint32_t)kChunk / 64; ++sl) {
+            const uint32_t idx = sl * 64 + lane;
+            if (sl * 64 >= m) break;
+            const bool v = idx < m;
+            const Rec r = S.stage[idx];
+            const uint32_t lim = Codec::limiter_of(r);
+            const DevLimiter& LL = L;
+            (void)lim;
+            const uint32_t reg = LL.region_base +
+                                 region_local(r.h, a.shard_bits, LL.region_bits);
+            const bool mine = v && (reg & (kRegionsPerBin - 1)) == w;
+            const uint64_t bal = __ballot(mine);
+            if (mine) {
+                const uint32_t k = (head + count + popc_below(bal)) % kRing;
+                S.ring[w][k] = r;
+                S.ring_pos[w][k] = c0 + idx;
             }
+            count += (uint32_t)__popcll(bal);
             wave_fence();
-            if (need && atomicCAS(&s_occ[cand], 0u, 1u) == 0u) {
-                s_tag[cand] = q.h; s_a[cand] = 0; s_b[cand] = 0; s_c[cand] = 0;
-                slot = (int32_t)cand;
-                need = false;
+            if (count >= 64) {
+                wave_apply<Codec, Res, TOK>(a, S, L, w, lane, head, 64, base, pad, n_allowed,
+                                            n_invalid, n_caperr);
+                head = (head + 64) % kRing;
+                count -= 64;
             }
-            wave_fence();
-            if (!__any(need)) break;
         }
-        if (failed) {
-            out = pack_result(false, kRemError);
-            ++n_caperr;
-        }
-        if (slot >= 0) atomicOr(&s_occ[slot], 2u);
-        // ---- apply in arrival order: per round, the first state-changing request of
-        // each key applies; the key's earlier (non-mutating) requests are final.
-        const uint64_t peers = wave_match((uint32_t)slot, kRegionBits, slot >= 0);
-        bool pending = slot >= 0;
-        while (__any(pending)) {
-            Outcome o{};
-            if (pending) {
-                o = tb ? tb_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot])
-                       : sw_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot]);
-            }
-            const uint64_t mut = __ballot(pending && o.mutate) & peers;
-            const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
-            if (pending && lane <= fm) {
-                if (lane == fm) { s_a[slot] = o.a; s_b[slot] = o.b; s_c[slot] = o.c; }
-                out = pack_result(o.allowed, o.remaining);
-                otok = o.tokens;
-                n_allowed += o.allowed ? 1u : 0u;
-                pending = false;
-            }
-            wave_fence();
-        }
-        const uint32_t w = valid ? j : pad;
-        res[w] = (Res)out;
-        if (TOK) a.tok[w] = otok;
     }
+    if (count > 0)
+        wave_apply<Codec, Res, TOK>(a, S, L, w, lane, head, count, base, pad, n_allowed,
+                                    n_invalid, n_caperr);
+    wave_fence();
     // ---- write the region back (free slots as zeros)
     uint32_t touched = 0;
-    for (uint32_t s = lane; s < S; s += 64) {
-        const uint32_t o = s_occ[s];
+    for (uint32_t s = lane; s < NS; s += 64) {
+        const uint32_t o = S.occ[w][s];
         Slot v;
-        if (o & 1u) { v.tag = s_tag[s]; v.a = s_a[s]; v.b = s_b[s]; v.c = s_c[s]; }
+        if (o & 1u) { v.tag = S.tag[w][s]; v.a = S.sa[w][s]; v.b = S.sb[w][s]; v.c = S.sc[w][s]; }
         else { v.tag = 0; v.a = 0; v.b = 0; v.c = 0; }
         tab[s] = v;
         touched += (o >> 1) & 1u;
@@ -456,19 +551,28 @@ __global__ __launch_bounds__(kRegionThreads) void k_region(RegionArgs a) {
         touched += __shfl_xor(touched, off, 64);
     }
     if (lane == 0) {
-        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
-        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
-        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
-        atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
-        atomicAdd(&a.ctl->regions, 1ULL);
+        atomicAdd(&S.stat[0], n_allowed);
+        atomicAdd(&S.stat[1], n_invalid);
+        atomicAdd(&S.stat[2], n_caperr);
+        atomicAdd(&S.stat[3], touched);
+    }
+    __syncthreads();
+    if (t == 0) {
+        atomicAdd(&a.ctl->allowed, (unsigned long long)S.stat[0]);
+        if (S.stat[1]) atomicAdd(&a.ctl->invalid, (unsigned long long)S.stat[1]);
+        if (S.stat[2]) atomicAdd(&a.ctl->cap_err, (unsigned long long)S.stat[2]);
+        atomicAdd(&a.ctl->distinct, (unsigned long long)S.stat[3]);
+        atomicAdd(&a.ctl->regions, (unsigned long long)kRegionsPerBin);
     }
 }
 
 // ------------------------------------------------------------------ 5. unpermute
 template <class Res>
 __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
-    const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
-    const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t it = 0;; ++it) {
+    const uint32_t tile = tile_at(it);
+    if (tile >= a.n_tiles) break;
     const Res* __restrict__ res = (const Res*)a.res;
     const uint32_t* __restrict__ pos0 = a.pos0;
     const uint32_t* __restrict__ pos1 = a.pos1;
@@ -487,8 +591,13 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
 #pragma unroll
             for (int k = 0; k < B; ++k) p[k] = pos1[p[k]];
         }
+        if (a.ablate & kAblNoGather) {
 #pragma unroll
-        for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+            for (int k = 0; k < B; ++k) v[k] = (Res)p[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+        }
 #pragma unroll
         for (int k = 0; k < B; ++k) {
             const uint32_t i = tile * (uint32_t)kTile + (uint32_t)(r0 + k) * kTileThreads + t;
@@ -499,6 +608,7 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
             }
         }
     }
+  }
 }
 
 __global__ void k_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n) {
@@ -617,8 +727,19 @@ __global__ __launch_bounds__(kTileThreads) void k_owner_scatter(const uint64_t* 
 // ------------------------------------------------------------------ launchers
 static inline uint32_t tiles_for(uint32_t n) { return (n + kTile - 1) / kTile; }
 
+static uint32_t persistent_grid(uint32_t n_tiles, uint32_t per_cu) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return std::max<uint32_t>(1u, std::min<uint32_t>(n_tiles, (uint32_t)cus * per_cu));
+}
+
 hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
-    dim3 grid(a.n_tiles), block(kTileThreads);
+    dim3 grid(persistent_grid(a.n_tiles, 2)), block(kTileThreads);
     if (raw) {
         if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_upsweep<CodecC, true>), grid, block, 0, s, a);
@@ -630,7 +751,7 @@ hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s)
 }
 
 hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
-    dim3 grid(a.n_tiles), block(kTileThreads);
+    dim3 grid(persistent_grid(a.n_tiles, 1)), block(kTileThreads);
     if (raw) {
         if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, 0, s, a);
@@ -660,8 +781,9 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
 
 template <class Codec, class Res>
 static void region_launch(const RegionArgs& a, hipStream_t s) {
-    if (a.tok) hipLaunchKernelGGL((k_region<Codec, Res, true>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
-    else hipLaunchKernelGGL((k_region<Codec, Res, false>), dim3(a.n_regions), dim3(kRegionThreads), 0, s, a);
+    const dim3 g(a.n_regions / kRegionsPerBin), b(kBinThreads);
+    if (a.tok) hipLaunchKernelGGL((k_bin<Codec, Res, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((k_bin<Codec, Res, false>), g, b, 0, s, a);
 }
 
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
@@ -673,7 +795,7 @@ hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStrea
 }
 
 hipError_t launch_unpermute(const UnpermArgs& a, int res_bytes, hipStream_t s) {
-    dim3 g(a.n_tiles), b(kTileThreads);
+    dim3 g(persistent_grid(a.n_tiles, 1)), b(kTileThreads);
     if (res_bytes == 8) hipLaunchKernelGGL(k_unpermute<uint64_t>, g, b, 0, s, a);
     else if (res_bytes == 1) hipLaunchKernelGGL(k_unpermute<uint8_t>, g, b, 0, s, a);
     else if (res_bytes == 2) hipLaunchKernelGGL(k_unpermute<uint16_t>, g, b, 0, s, a);

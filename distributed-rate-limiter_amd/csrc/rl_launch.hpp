@@ -7,6 +7,19 @@
 
 namespace rl {
 
+// Ablation bits (rl_tune "ablate"): timing experiments only; results are wrong when set.
+enum : uint32_t {
+    kAblNoRecStore = 1u << 0,    // scatter: skip the record store
+    kAblSeqRecStore = 1u << 1,   // scatter: store records at their input index (coalesced)
+    kAblNoMatch = 1u << 2,       // scatter: skip the ballot match (rank 0 for every lane)
+    kAblNoPosStore = 1u << 3,    // scatter: skip pos_out
+    kAblNoBarrier = 1u << 4,     // scatter: skip the two per-round barriers
+    kAblNoStep = 1u << 8,        // region: skip the per-request semantics
+    kAblNoProbe = 1u << 9,       // region: slot = home (no lookup / insert)
+    kAblNoRounds = 1u << 10,     // region: one round, no peer match
+    kAblNoGather = 1u << 16,     // unpermute: skip the res gather
+};
+
 // Per-batch device control block (written by kernels, read by later kernels/host).
 struct BatchCtl {
     int64_t base_ms;           // compact records: now_ms = base_ms + now_rel
@@ -43,19 +56,22 @@ struct PartArgs {
     const uint32_t* bin_base;  // [bins]
     uint32_t* region_count;    // nullable: full-region histogram (multi-pass only)
     BatchCtl* ctl;
+    uint32_t ablate;           // rl_tune("ablate"): measurement-only variants (0 = product)
 };
 
 struct RegionArgs {
     const void* rec;           // records in region order
-    const uint32_t* rstart;    // [P]
-    const uint32_t* rcount;    // [P]
+    const uint32_t* rstart;    // [bins] first record of each bin
+    const uint32_t* rcount;    // [bins]
     const uint8_t* region_lim; // [P]
     const DevLimiter* lims;
     void* res;                 // packed results in region order (u32 compact, u64 wide)
     double* tok;               // nullable: TB fp64 balances in region order
     BatchCtl* ctl;
-    uint32_t n_regions;
+    uint32_t n_regions;        // multiple of kRegionsPerBin; one workgroup per bin
     uint32_t n_total;          // batch size: res/tok carry 64 padding entries past it
+    int32_t shard_bits;
+    uint32_t ablate;
 };
 
 struct UnpermArgs {
@@ -68,6 +84,7 @@ struct UnpermArgs {
     double* tokens_out;        // nullable
     uint32_t n;
     uint32_t n_tiles;
+    uint32_t ablate;
 };
 
 struct SynthArgs {

@@ -1,0 +1,167 @@
+// ratelimiter.cpp — see ratelimiter.hpp.
+#include "ratelimiter.hpp"
+
+#include <cstring>
+
+namespace ratelimiter {
+
+uint64_t keyHash(const std::string& key) {
+    uint64_t h = 0xcbf29ce484222325ULL;                 // FNV-1a 64
+    for (unsigned char c : key) {
+        h ^= c;
+        h *= 0x100000001b3ULL;
+    }
+    h ^= h >> 30; h *= 0xbf58476d1ce4e5b9ULL;           // splitmix64 finaliser
+    h ^= h >> 27; h *= 0x94d049bb133111ebULL;
+    h ^= h >> 31;
+    return h;
+}
+
+int64_t systemNanos() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+GpuEngine::GpuEngine(const Options& o) {
+    rl_opts opts{};
+    opts.device = o.device;
+    opts.max_batch = o.maxBatch;
+    opts.default_capacity = o.defaultCapacity;
+    opts.shard_count = 1;
+    int st = rl_create(&opts, &e_);
+    if (st != RL_OK) throw StorageException(std::string("rl_create: ") + rl_strerror(st), st);
+}
+
+GpuEngine::~GpuEngine() { rl_destroy(e_); }
+
+uint16_t GpuEngine::addLimiter(int algo, const RateLimitConfig& c) {
+    rl_limiter_config lc{};
+    lc.algo = algo;
+    lc.max_permits = c.maxPermits;
+    lc.window_ms = c.windowMs;
+    lc.refill_per_s = c.refillRate;
+    lc.capacity = c.expectedKeys;
+    uint16_t id = 0;
+    int st = rl_add_limiter_ex(e_, &lc, &id);
+    if (st == RL_E_INVALID_ARG)
+        throw IllegalArgumentException(std::string("limiter configuration rejected: ") + rl_strerror(st));
+    if (st != RL_OK) throw StorageException(std::string("rl_add_limiter: ") + rl_strerror(st), st);
+    return id;
+}
+
+GpuRateLimiter::GpuRateLimiter(std::shared_ptr<GpuEngine> engine, Algorithm algo,
+                               const RateLimitConfig& cfg, Clock clock, int batchWindowMicros)
+    : allowedRequests(algo == Algorithm::TokenBucket ? "ratelimiter.tokenbucket.allowed"
+                                                      : "ratelimiter.requests.allowed"),
+      rejectedRequests(algo == Algorithm::TokenBucket ? "ratelimiter.tokenbucket.rejected"
+                                                       : "ratelimiter.requests.rejected"),
+      engine_(std::move(engine)), algo_(algo), cfg_(cfg), clock_(std::move(clock)),
+      windowMicros_(batchWindowMicros) {
+    cfg_.validate();                                    // SlidingWindowRateLimiter.java:51
+    if (algo == Algorithm::TokenBucket && !(cfg_.refillRate > 0))
+        throw IllegalArgumentException(                // TokenBucketRateLimiter.java:77-79
+            "Token bucket requires positive refillRate. Use RateLimitConfig.builder().refillRate(...)");
+    id_ = engine_->addLimiter((int)algo, cfg_);
+}
+
+GpuRateLimiter::~GpuRateLimiter() = default;
+
+void GpuRateLimiter::checkStatus(int st, const char* where) {
+    if (st == RL_OK || st == RL_E_INVALID_REQUEST) return;
+    if (st == RL_E_INVALID_ARG) throw IllegalArgumentException(std::string(where) + ": " + rl_strerror(st));
+    throw StorageException(std::string(where) + ": " + rl_strerror(st), st);
+}
+
+// Leader-based micro-batcher: the first caller that finds no flush in progress waits
+// `windowMicros_` for company, then runs every queued request as ONE engine batch in
+// queue (arrival) order; the others sleep until their result is filled in.
+void GpuRateLimiter::submit(Pending& p) {
+    std::unique_lock<std::mutex> lk(mu_);
+    queue_.push_back(&p);
+    while (!p.done) {
+        if (!flushing_) {
+            flushing_ = true;
+            if (windowMicros_ > 0) {
+                lk.unlock();
+                std::this_thread::sleep_for(std::chrono::microseconds(windowMicros_));
+                lk.lock();
+            }
+            flushLocked(lk);
+            flushing_ = false;
+            cv_.notify_all();
+        } else {
+            cv_.wait(lk);
+        }
+    }
+    if (p.status != RL_OK && p.status != RL_E_INVALID_REQUEST) checkStatus(p.status, "tryAcquire");
+}
+
+void GpuRateLimiter::flushLocked(std::unique_lock<std::mutex>& lk) {
+    std::vector<Pending*> batch;
+    batch.swap(queue_);
+    lk.unlock();
+    const size_t n = batch.size();
+    std::vector<uint64_t> k(n);
+    std::vector<int32_t> pm(n);
+    std::vector<int64_t> t(n), rem(n);
+    std::vector<uint16_t> lim(n, id_);
+    std::vector<uint8_t> op(n), al(n);
+    for (size_t i = 0; i < n; ++i) {
+        k[i] = batch[i]->key; pm[i] = batch[i]->permits; t[i] = batch[i]->now; op[i] = batch[i]->op;
+    }
+    int st = rl_execute_batch(engine_->handle(), n, k.data(), pm.data(), t.data(), lim.data(),
+                              op.data(), al.data(), rem.data(), nullptr);
+    lk.lock();
+    for (size_t i = 0; i < n; ++i) {
+        batch[i]->allowed = al[i];
+        batch[i]->remaining = rem[i];
+        batch[i]->status = st;
+        batch[i]->done = true;
+    }
+}
+
+bool GpuRateLimiter::tryAcquire(const std::string& key, int permits) {
+    if (permits <= 0) throw IllegalArgumentException("permits must be positive");  // :87-89 / :106-108
+    Pending p{keyHash(key), permits, clock_(), RL_OP_ACQUIRE};
+    submit(p);
+    if (p.allowed) allowedRequests.increment();
+    else rejectedRequests.increment();
+    return p.allowed != 0;
+}
+
+int64_t GpuRateLimiter::getAvailablePermits(const std::string& key) {
+    Pending p{keyHash(key), 1, clock_(), RL_OP_PEEK};
+    submit(p);
+    return p.remaining;
+}
+
+void GpuRateLimiter::reset(const std::string& key) {
+    Pending p{keyHash(key), 1, clock_(), RL_OP_RESET};
+    submit(p);
+}
+
+void GpuRateLimiter::tryAcquireBatch(size_t n, const uint64_t* keyHash, const int32_t* permits,
+                                     const int64_t* nowNanos, bool* allowed, int64_t* remaining) {
+    if (n == 0) return;
+    std::vector<uint16_t> lim(n, id_);
+    std::vector<uint8_t> al(n);
+    std::vector<int64_t> rem(n);
+    int st;
+    {
+        std::lock_guard<std::mutex> lk(mu_);        // keep arrival order with single calls
+        st = rl_try_acquire_batch(engine_->handle(), n, keyHash, permits, nowNanos, lim.data(),
+                                  al.data(), rem.data(), nullptr);
+    }
+    checkStatus(st, "tryAcquireBatch");
+    uint64_t ok = 0;
+    for (size_t i = 0; i < n; ++i) {
+        allowed[i] = al[i] != 0;
+        ok += al[i];
+        if (remaining) remaining[i] = rem[i];
+    }
+    allowedRequests.increment(ok);
+    rejectedRequests.increment(n - ok);
+}
+
+}  // namespace ratelimiter

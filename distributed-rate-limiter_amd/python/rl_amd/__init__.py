@@ -31,13 +31,14 @@ OP_ACQUIRE, OP_PEEK, OP_RESET = 0, 1, 2
 REM_UNKNOWN, REM_INVALID, REM_ERROR = -1, -2, -3
 OPT_STAGE_TIMING = 1
 REGION_SLOTS = 256          # kRegionSlots in csrc/rl_device.hpp (state slots per region)
+MIN_REGIONS = 8             # kRegionsPerBin: every limiter has at least one bin of regions
 DIST_UNIFORM, DIST_ZIPF = 0, 1
 
 EXPORTS = [
     "rl_create", "rl_destroy", "rl_add_limiter", "rl_add_limiter_ex", "rl_try_acquire_batch",
     "rl_execute_batch", "rl_execute_batch_device", "rl_last_status", "rl_available", "rl_reset",
     "rl_batch_stats_get", "rl_stage_times", "rl_sync", "rl_strerror", "rl_abi_version",
-    "rl_owner_of", "rl_route_partition", "rl_synth_trace_device",
+    "rl_owner_of", "rl_route_partition", "rl_synth_trace_device", "rl_tune",
 ]
 
 
@@ -117,6 +118,7 @@ def lib():
     L.rl_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p),
                                  ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     L.rl_sync.argtypes = [vp]
+    L.rl_tune.argtypes = [vp, ctypes.c_char_p, i64]
     L.rl_strerror.argtypes = [ctypes.c_int]
     L.rl_strerror.restype = ctypes.c_char_p
     L.rl_owner_of.argtypes = [ctypes.c_uint64, u16, u32]
@@ -266,6 +268,11 @@ class Engine:
         ms = (ctypes.c_float * 16)()
         k = self._L.rl_stage_times(self._h, names, ms, 16)
         return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+    def tune(self, key: str, value: int):
+        st = self._L.rl_tune(self._h, key.encode(), int(value))
+        if st != RL_OK:
+            raise RlError(st, "rl_tune")
 
     def sync(self):
         st = self._L.rl_sync(self._h)

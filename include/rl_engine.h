@@ -174,6 +174,9 @@ int  rl_batch_stats_get(rl_engine* e, rl_batch_stats* out);
  * names[i] are static strings. Returns the number of stages written (<= cap). */
 int  rl_stage_times(rl_engine* e, const char** names, float* ms, int cap);
 int  rl_sync(rl_engine* e);
+/* Tuning / measurement knobs (not needed by callers): "ablate" = bit set of
+ * measurement-only kernel variants whose results are NOT valid (0 = product path). */
+int  rl_tune(rl_engine* e, const char* key, int64_t value);
 const char* rl_strerror(int status);
 int  rl_abi_version(void);
 

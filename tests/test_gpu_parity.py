@@ -139,7 +139,7 @@ def test_ttl_reclamation_reuses_slots():
     # (two waves together would not fit).
     lims = [[rl_amd.TB, 5, 1000, 2.0, 1], [rl_amd.SW, 5, 1000, 0.0, 1]]
     parts = []
-    nk = int(rl_amd.REGION_SLOTS * 0.6)
+    nk = int(rl_amd.REGION_SLOTS * rl_amd.MIN_REGIONS * 0.6)
     for w in range(3):
         k = rl_amd.mix64(np.arange(nk, dtype=np.uint64) + np.uint64(w * 1000))
         k = np.repeat(k, 3)
@@ -158,12 +158,19 @@ def test_ttl_reclamation_reuses_slots():
 
 def test_capacity_overflow_reported():
     e = rl_amd.Engine(max_batch=1 << 16, capacity=1)
-    e.add_limiter(rl_amd.TB, 5, 60000, 1.0, capacity=1)     # one region of REGION_SLOTS slots
-    keys = rl_amd.mix64(np.arange(2000, dtype=np.uint64))
-    a, r, t, st = e.execute(keys, np.ones(2000, np.int32), np.full(2000, T0 * NS, np.int64))
+    e.add_limiter(rl_amd.TB, 5, 60000, 1.0, capacity=1)     # MIN_REGIONS regions
+    n = 3000
+    keys = rl_amd.mix64(np.arange(n, dtype=np.uint64))
+    a, r, t, st = e.execute(keys, np.ones(n, np.int32), np.full(n, T0 * NS, np.int64))
     assert st == rl_amd.RL_E_CAPACITY
-    assert (r == rl_amd.REM_ERROR).sum() == 2000 - rl_amd.REGION_SLOTS
-    assert a.sum() == rl_amd.REGION_SLOTS
+    # region = top log2(MIN_REGIONS) bits of mix64(key); each holds REGION_SLOTS keys
+    bits = rl_amd.MIN_REGIONS.bit_length() - 1
+    region = (rl_amd.mix64(keys) >> np.uint64(64 - bits)).astype(np.int64)
+    per = np.bincount(region, minlength=rl_amd.MIN_REGIONS)
+    overflow = np.maximum(per - rl_amd.REGION_SLOTS, 0).sum()
+    assert overflow > 0
+    assert (r == rl_amd.REM_ERROR).sum() == overflow
+    assert a.sum() == n - overflow
 
 
 def test_wide_records_large_max():
