@@ -130,8 +130,12 @@ def main():
     steps, warm = args.steps, args.warmup
     total_steps = steps + warm
 
-    eng = rl_amd.Engine(device=local, max_batch=n * (2 if ws > 1 else 1), capacity=cfg["capacity"],
-                        stage_timing=True, shard_index=rank, shard_count=ws)
+    # weak scaling: each shard owns 1/ws of the keys but sees ws x n requests' worth of
+    # key space across ranks, i.e. the same number of requests per GPU; a shard's table
+    # is sized for its share of the global key population.
+    eng = rl_amd.Engine(device=local, max_batch=n * (2 if ws > 1 else 1),
+                        capacity=cfg["capacity"] * ws, stage_timing=True, shard_index=rank,
+                        shard_count=ws)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)
 
@@ -154,8 +158,8 @@ def main():
     torch.cuda.synchronize()
 
     if ws > 1:
-        from rl_amd.router import Router
-        router = Router(eng, ws, rank, n, dev)
+        from rl_amd.router import DeviceOps, Router
+        router = Router(DeviceOps(eng, ws, dev, n), ws, rank)
 
         def step(s):
             router.step(*inputs[s], allowed, remaining)

@@ -657,6 +657,37 @@ extern "C" int rl_route_partition(rl_engine* e, size_t n, const uint64_t* key_ha
     return RL_OK;
 }
 
+extern "C" int rl_route_pack(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key,
+                             const int32_t* permits, const int64_t* now_ns, const uint16_t* limiter,
+                             uint64_t* key_out, int32_t* permits_out, int64_t* now_out,
+                             uint16_t* limiter_out, void* stream) {
+    if (!e || (n && (!perm || !key || !permits || !now_ns || !key_out || !permits_out || !now_out)))
+        return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_pack((uint32_t)n, perm, key, permits, now_ns, limiter, key_out, permits_out,
+                             now_out, limiter_out, s));
+    return RL_OK;
+}
+
+extern "C" int rl_route_fold(rl_engine* e, size_t n, const uint8_t* allowed, const int64_t* remaining,
+                             int64_t* packed, void* stream) {
+    if (!e || (n && (!allowed || !remaining || !packed))) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_fold((uint32_t)n, allowed, remaining, packed, s));
+    return RL_OK;
+}
+
+extern "C" int rl_route_unpack(rl_engine* e, size_t n, const uint32_t* perm, const int64_t* packed,
+                               uint8_t* allowed, int64_t* remaining, void* stream) {
+    if (!e || (n && (!perm || !packed || !allowed || !remaining))) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_unpack((uint32_t)n, perm, packed, allowed, remaining, s));
+    return RL_OK;
+}
+
 extern "C" int rl_synth_trace_device(rl_engine* e, const rl_trace_spec* sp, size_t n,
                                      uint64_t* key_hash, int32_t* permits, int64_t* now_ns,
                                      uint16_t* limiter, void* stream) {

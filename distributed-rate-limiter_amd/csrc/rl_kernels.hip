@@ -724,6 +724,47 @@ __global__ __launch_bounds__(kTileThreads) void k_owner_scatter(const uint64_t* 
     }
 }
 
+// ------------------------------------------------------------------ route pack / unpack
+// Multi-GPU routing: gather requests into owner order (perm from k_owner_scatter) before
+// the all-to-all, and scatter the returned decisions back to arrival order after it.
+__global__ __launch_bounds__(256) void k_route_pack(uint32_t n, const uint32_t* __restrict__ perm,
+                                                    const uint64_t* __restrict__ key,
+                                                    const int32_t* __restrict__ permits,
+                                                    const int64_t* __restrict__ now,
+                                                    const uint16_t* __restrict__ lim,
+                                                    uint64_t* __restrict__ key_o,
+                                                    int32_t* __restrict__ permits_o,
+                                                    int64_t* __restrict__ now_o,
+                                                    uint16_t* __restrict__ lim_o) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = perm[j];
+    key_o[j] = key[i];
+    permits_o[j] = permits[i];
+    now_o[j] = now[i];
+    if (lim_o) lim_o[j] = lim ? lim[i] : 0;
+}
+
+// decisions travel as one int64 per request: remaining * 2 + allowed
+__global__ __launch_bounds__(256) void k_route_fold(uint32_t n, const uint8_t* __restrict__ allowed,
+                                                    const int64_t* __restrict__ remaining,
+                                                    int64_t* __restrict__ packed) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) packed[j] = (int64_t)((uint64_t)remaining[j] << 1) | (int64_t)(allowed[j] & 1u);
+}
+
+__global__ __launch_bounds__(256) void k_route_unpack(uint32_t n, const uint32_t* __restrict__ perm,
+                                                      const int64_t* __restrict__ packed,
+                                                      uint8_t* __restrict__ allowed,
+                                                      int64_t* __restrict__ remaining) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t v = packed[j];
+    const uint32_t i = perm[j];
+    allowed[i] = (uint8_t)(v & 1);
+    remaining[i] = v >> 1;
+}
+
 // ------------------------------------------------------------------ launchers
 static inline uint32_t tiles_for(uint32_t n) { return (n + kTile - 1) / kTile; }
 
@@ -829,6 +870,31 @@ hipError_t launch_owner_partition(const uint64_t* key, uint32_t n, uint32_t shar
     hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, counts_dev, base, shard_count);
     hipLaunchKernelGGL(k_owner_scatter, dim3(nt), dim3(kTileThreads), 0, s, key, n, sbits, nt,
                        counts, base, perm);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_pack(uint32_t n, const uint32_t* perm, const uint64_t* key,
+                             const int32_t* permits, const int64_t* now, const uint16_t* lim,
+                             uint64_t* key_o, int32_t* permits_o, int64_t* now_o, uint16_t* lim_o,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_route_pack, dim3((n + 255) / 256), dim3(256), 0, s, n, perm, key, permits,
+                       now, lim, key_o, permits_o, now_o, lim_o);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_fold(uint32_t n, const uint8_t* allowed, const int64_t* remaining,
+                             int64_t* packed, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_route_fold, dim3((n + 255) / 256), dim3(256), 0, s, n, allowed, remaining, packed);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_unpack(uint32_t n, const uint32_t* perm, const int64_t* packed,
+                               uint8_t* allowed, int64_t* remaining, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_route_unpack, dim3((n + 255) / 256), dim3(256), 0, s, n, perm, packed,
+                       allowed, remaining);
     return hipGetLastError();
 }
 

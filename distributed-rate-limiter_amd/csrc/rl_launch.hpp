@@ -122,4 +122,13 @@ hipError_t launch_owner_partition(const uint64_t* key, uint32_t n, uint32_t shar
                                   uint32_t* perm, uint32_t* counts_dev, uint32_t* scratch,
                                   hipStream_t s);
 
+hipError_t launch_route_pack(uint32_t n, const uint32_t* perm, const uint64_t* key,
+                             const int32_t* permits, const int64_t* now, const uint16_t* lim,
+                             uint64_t* key_o, int32_t* permits_o, int64_t* now_o, uint16_t* lim_o,
+                             hipStream_t s);
+hipError_t launch_route_fold(uint32_t n, const uint8_t* allowed, const int64_t* remaining,
+                             int64_t* packed, hipStream_t s);
+hipError_t launch_route_unpack(uint32_t n, const uint32_t* perm, const int64_t* packed,
+                               uint8_t* allowed, int64_t* remaining, hipStream_t s);
+
 }  // namespace rl

@@ -39,6 +39,7 @@ EXPORTS = [
     "rl_execute_batch", "rl_execute_batch_device", "rl_last_status", "rl_available", "rl_reset",
     "rl_batch_stats_get", "rl_stage_times", "rl_sync", "rl_strerror", "rl_abi_version",
     "rl_owner_of", "rl_route_partition", "rl_synth_trace_device", "rl_tune",
+    "rl_route_pack", "rl_route_fold", "rl_route_unpack",
 ]
 
 
@@ -124,6 +125,9 @@ def lib():
     L.rl_owner_of.argtypes = [ctypes.c_uint64, u16, u32]
     L.rl_owner_of.restype = u32
     L.rl_route_partition.argtypes = [vp, sz, vp, vp, u32, vp, vp, vp]
+    L.rl_route_pack.argtypes = [vp, sz] + [vp] * 10
+    L.rl_route_fold.argtypes = [vp, sz] + [vp] * 4
+    L.rl_route_unpack.argtypes = [vp, sz] + [vp] * 5
     L.rl_synth_trace_device.argtypes = [vp, ctypes.POINTER(TraceSpec), sz, vp, vp, vp, vp, vp]
     _lib = L
     return L
@@ -286,6 +290,25 @@ class Engine:
         if st != RL_OK:
             raise RlError(st, "rl_route_partition")
         return counts
+
+    def route_pack(self, n, perm, key, permits, now, limiter, key_o, permits_o, now_o, limiter_o,
+                   stream=None):
+        st = self._L.rl_route_pack(self._h, n, _p(perm), _p(key), _p(permits), _p(now),
+                                   _p(limiter), _p(key_o), _p(permits_o), _p(now_o),
+                                   _p(limiter_o), _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_pack")
+
+    def route_fold(self, n, allowed, remaining, packed, stream=None):
+        st = self._L.rl_route_fold(self._h, n, _p(allowed), _p(remaining), _p(packed), _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_fold")
+
+    def route_unpack(self, n, perm, packed, allowed, remaining, stream=None):
+        st = self._L.rl_route_unpack(self._h, n, _p(perm), _p(packed), _p(allowed), _p(remaining),
+                                     _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_unpack")
 
     def synth_trace(self, n, keys, permits, now_ns, limiter, *, seed, n_keys, dist=DIST_UNIFORM,
                     zipf_s=1.1, permits_max=4, t0_ns=1_700_000_000_000 * 1_000_000,

@@ -188,6 +188,17 @@ uint32_t rl_owner_of(uint64_t key_hash, uint16_t limiter, uint32_t shard_count);
 int  rl_route_partition(rl_engine* e, size_t n, const uint64_t* key_hash,
                         const uint16_t* limiter, uint32_t shard_count,
                         uint32_t* perm, uint64_t* counts_host, void* stream);
+/* out[j] = in[perm[j]] for the four request arrays (limiter / limiter_out nullable). */
+int  rl_route_pack(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key_hash,
+                   const int32_t* permits, const int64_t* now_ns, const uint16_t* limiter,
+                   uint64_t* key_out, int32_t* permits_out, int64_t* now_out,
+                   uint16_t* limiter_out, void* stream);
+/* packed[j] = remaining[j] * 2 + allowed[j] (one int64 per decision for the return trip). */
+int  rl_route_fold(rl_engine* e, size_t n, const uint8_t* allowed, const int64_t* remaining,
+                   int64_t* packed, void* stream);
+/* allowed[perm[j]], remaining[perm[j]] = unfold(packed[j]). */
+int  rl_route_unpack(rl_engine* e, size_t n, const uint32_t* perm, const int64_t* packed,
+                     uint8_t* allowed, int64_t* remaining, void* stream);
 
 /* ---- synthetic traces (bench / tests; deterministic in (seed, index)) ------ */
 #define RL_DIST_UNIFORM 0
