@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="requests per GPU per step (override)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    ap.add_argument("--tune", action="append", default=[],
+                    help="engine knob key=value (rl_tune), e.g. bin_shift=0")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -138,6 +140,9 @@ def main():
                         shard_count=ws)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)
+    for kv in args.tune:
+        k, v = kv.split("=")
+        eng.tune(k, int(v))
 
     dev = torch.device("cuda", local)
     n_global_total = total_steps * ws * n
@@ -146,7 +151,7 @@ def main():
         keys = torch.empty(n, dtype=torch.int64, device=dev)
         permits = torch.empty(n, dtype=torch.int32, device=dev)
         now = torch.empty(n, dtype=torch.int64, device=dev)
-        eng.synth_trace(n, keys, permits, now, None, seed=cfg["seed"], n_keys=cfg["n_keys"],
+        eng.synth_trace(n, keys, permits, now, None, seed=cfg["seed"], n_keys=cfg["n_keys"] * ws,
                         dist=cfg["dist"], zipf_s=cfg.get("zipf_s", 1.1),
                         permits_max=cfg["permits_max"], t0_ns=T0_NS,
                         span_ns=cfg["span_ns"] * total_steps,
@@ -220,7 +225,7 @@ def main():
         "dtype": "f64" if cfg["limiters"][0][0] == rl_amd.TB else "int64+f64",
         "data": "synthetic (deterministic splitmix64 trace generated on device)",
         "config": {"workload": f"{args.config}: {cfg['desc']}", "requests_per_gpu_per_step": n,
-                   "n_keys": cfg["n_keys"], "parallelism": f"key-hash shards x{ws}"
+                   "n_keys": cfg["n_keys"] * ws, "parallelism": f"key-hash shards x{ws}"
                    + (" + RCCL all-to-all routing" if ws > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom,

@@ -34,10 +34,8 @@ constexpr int64_t kRemError = -3;     // state-table region full
 // inside each XCD's 4 MB L2.
 constexpr int kRegionSlots = 256;                 // slots per region (load <= ~0.5)
 constexpr int kRegionBits = 8;
-constexpr int kRegionsPerBin = 8;                 // = waves per bin workgroup
-constexpr int kBinShift = 3;
-constexpr int kBinThreads = 64 * kRegionsPerBin;  // 512
-constexpr int kChunk = kBinThreads;               // records staged per step
+constexpr int kRegionsPerBin = 8;                 // regions per bin (bin_shift = 3) ...
+constexpr int kBinShift = 3;                      // ... every limiter has >= 8 regions
 constexpr int kRing = 128;                        // per-wave pending ring (< 64 + 64 entries)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
@@ -47,7 +45,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kTileThreads = 256;
 constexpr int kTileItems = 256;
 constexpr int kTile = kTileThreads * kTileItems;  // 65536 requests per tile
-constexpr int kMaxDigitBits = 10;                 // <= 1024 bins per pass
+constexpr int kMaxDigitBits = 13;                 // <= 8192 bins per pass
 
 // Compact record field limits.
 constexpr uint32_t kPermitBits = 22;

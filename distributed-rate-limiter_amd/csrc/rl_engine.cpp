@@ -105,6 +105,7 @@ struct rl_engine {
     int last_status = RL_OK;
     uint64_t last_n = 0;
     uint32_t ablate = 0;                    // rl_tune("ablate"), measurement only
+    int bin_shift = 0;                      // rl_tune("bin_shift"): 0 or 3 (regions per bin 1/8)
 };
 
 #define HIP_OK(x)                                                      \
@@ -361,7 +362,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     const int res_bytes = res_bytes_for(max_any, wide);
     const uint32_t nt = (uint32_t)((n + kTile - 1) / kTile);
-    const uint32_t n_bins = e->n_regions / kRegionsPerBin;
+    const int bsh = e->bin_shift;
+    const uint32_t n_bins = e->n_regions >> bsh;
     const int bitsP = std::max(1, ceil_log2(n_bins));
     const int passes = bitsP <= kMaxDigitBits ? 1 : 2;
     if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
@@ -383,6 +385,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.n = (uint32_t)n; pa.n_tiles = nt; pa.n_lim = (uint32_t)e->lims.size();
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = e->d_ctl;
     pa.counts = e->counts; pa.bin_base = e->bin_base; pa.ablate = e->ablate;
+    pa.bin_shift = bsh;
     // ---- pass 0 (low digit) from the caller's arrays
     pa.digit_shift = 0; pa.digit_bits = d0;
     pa.region_count = nullptr;
@@ -432,7 +435,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.region_lim = e->d_region_lim;
     ra.lims = e->d_lims; ra.res = e->res; ra.tok = tokens_after ? e->tok : nullptr;
     ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
-    ra.shard_bits = e->shard_bits;
+    ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
     HIP_OK(launch_region(ra, wide, res_bytes, s));
     mark(e, 8);
     UnpermArgs ua{};
@@ -618,6 +621,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (!e || !key) return RL_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(e->mu);
     if (std::strcmp(key, "ablate") == 0) { e->ablate = (uint32_t)value; return RL_OK; }
+    if (std::strcmp(key, "bin_shift") == 0) {
+        if (value != 0 && value != kBinShift) return RL_E_INVALID_ARG;
+        e->bin_shift = (int)value;
+        return RL_OK;
+    }
     return RL_E_INVALID_ARG;
 }
 

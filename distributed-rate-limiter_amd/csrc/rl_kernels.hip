@@ -10,13 +10,12 @@
 //   3. k_scatter  : stable partition (wave ballot-match ranking) of the requests
 //                   into bin order, packed into 16-byte records.
 //   (1-3 repeat once more when a limiter set has > 1024 bins.)
-//   4. k_bin      : one 8-wave workgroup per bin, one WAVE per region. Each wave loads
-//                   its region's 256 state slots (8 KB) into LDS once; the bin's
-//                   records are staged through LDS 512 at a time in arrival order,
-//                   every wave compacts its own region's requests into a ring and
-//                   applies the reference semantics per key in order (deny never
-//                   mutates, so a 64-request group needs 1 + (#state changes of its
-//                   busiest key) rounds); the regions are written back once.
+//   4. k_regions  : one single-wave workgroup per REGION. The wave loads its region's
+//                   256 state slots (8 KB) into LDS once, streams its bin's records
+//                   in arrival order, keeps its region's requests in an LDS ring and
+//                   applies the reference semantics per key in order, 64 at a time
+//                   (deny never mutates, so a group needs 1 + (#state changes of its
+//                   busiest key) rounds); the region is written back once.
 //   5. k_unpermute: results back to the caller's order (allowed u8, remaining i64).
 //
 // Partition and unpermute grids are persistent and walk tiles XCD-aware: at any
@@ -113,7 +112,7 @@ __device__ inline uint32_t bin_of(const PartArgs& a, uint32_t i, const LimLds& L
         h = r->h;
         lim = Codec::limiter_of(*r);
     }
-    return (L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> kBinShift;
+    return (L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift;
 }
 
 // ------------------------------------------------------------------ 1. upsweep
@@ -286,12 +285,12 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                     const uint64_t k = ord_key(now_ms);
                     mn = k < mn ? k : mn;
                     mx = k > mx ? k : mx;
-                    d = (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> kBinShift)
+                    d = (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
                          >> a.digit_shift) & mask;
                 } else {
                     rec = in.rec;
                     const uint32_t lim = Codec::limiter_of(rec);
-                    d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> kBinShift)
+                    d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
                          >> a.digit_shift) & mask;
                 }
             }
@@ -342,79 +341,99 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     }
 }
 
-// ------------------------------------------------------------------ 4. bin / region
+// ------------------------------------------------------------------ 4. regions
+// One single-wave workgroup per REGION. The region's 256 slots (8 KB) live in the wave's
+// LDS for the whole batch. The wave streams its BIN's records (arrival order, 8
+// regions interleaved) 64 at a time, keeps the ones of its region in an LDS ring and
+// applies them 64 at a time. The 8 waves of a bin have block ids congruent mod 8 and
+// adjacent in dispatch order, i.e. they run together on one XCD, so the bin's stream is
+// fetched from HBM once and re-read from that XCD's L2. No barriers anywhere.
 __device__ inline void wave_fence() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }
 
-template <class Codec>
-struct BinLds {
-    using Rec = typename Codec::Rec;
-    uint64_t tag[kRegionsPerBin][kRegionSlots];
-    uint64_t sa[kRegionsPerBin][kRegionSlots];
-    uint64_t sb[kRegionsPerBin][kRegionSlots];
-    uint64_t sc[kRegionsPerBin][kRegionSlots];
-    uint32_t occ[kRegionsPerBin][kRegionSlots];   // bit0 occupied, bit1 touched by this batch
-    Rec stage[kChunk];                            // the bin's next records, arrival order
-    Rec ring[kRegionsPerBin][kRing];              // per-wave pending requests
-    uint32_t ring_pos[kRegionsPerBin][kRing];     // ... and their positions (result index)
-    uint32_t stat[4];
+// first probe position of a key inside its region (4-slot aligned: probing reads buckets)
+__device__ inline uint32_t slot_home(uint64_t h) { return (uint32_t)h & (kRegionSlots - 4); }
+
+struct RegionTable {
+    alignas(16) uint64_t tag[kRegionSlots];
+    uint64_t sa[kRegionSlots];
+    uint64_t sb[kRegionSlots];
+    uint64_t sc[kRegionSlots];
+    alignas(16) uint32_t occ[kRegionSlots];   // bit0 occupied, bit1 touched by this batch
 };
 
-// One wave applies up to 64 of its region's pending requests (ring[head..head+n)) in
-// arrival order against its LDS region image.
-template <class Codec, class Res, bool TOK>
-__device__ inline void wave_apply(const RegionArgs& a, BinLds<Codec>& S, const DevLimiter& L,
-                                  uint32_t w, uint32_t lane, uint32_t head, uint32_t n,
-                                  int64_t base, uint32_t pad, uint32_t& n_allowed,
-                                  uint32_t& n_invalid, uint32_t& n_caperr) {
+template <class Codec, bool RING>
+struct RegionLds : RegionTable {
     using Rec = typename Codec::Rec;
+    Rec ring[kRing];                  // this region's pending requests (bins of 8 regions)
+    uint32_t ring_pos[kRing];         // ... and their result index
+};
+template <class Codec>
+struct RegionLds<Codec, false> : RegionTable {};
+
+struct Applied {
+    uint32_t j;                       // result index (padding slot for idle lanes)
+    uint64_t out;                     // packed result
+    double tok;
+};
+
+// Apply one group of up to 64 requests (lane order = arrival order; `valid` lanes only).
+template <class Codec, class LdsT>
+__device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimiter& L,
+                                     uint32_t lane, const typename Codec::Rec& cur, bool valid,
+                                     uint32_t j, int64_t base, uint32_t pad, uint32_t& n_allowed,
+                                     uint32_t& n_invalid, uint32_t& n_caperr) {
     constexpr uint32_t NS = kRegionSlots;
-    uint64_t* s_tag = S.tag[w];
-    uint64_t* s_a = S.sa[w];
-    uint64_t* s_b = S.sb[w];
-    uint64_t* s_c = S.sc[w];
-    uint32_t* s_occ = S.occ[w];
     const bool tb = L.algo == kAlgoTB;
-    const bool valid = lane < n;
-    const uint32_t ri = (head + (valid ? lane : 0u)) % kRing;
-    const Rec cur = S.ring[w][ri];
-    const uint32_t j = valid ? S.ring_pos[w][ri] : pad;
+    Applied r;
+    r.j = valid ? j : pad;
     const Req q = Codec::dec(cur, base);
     const bool live = valid && !q.invalid;
-    uint64_t out = pack_result(false, kRemInvalid);
-    double otok = __builtin_nan("");
+    r.out = pack_result(false, kRemInvalid);
+    r.tok = __builtin_nan("");
     n_invalid += (valid && q.invalid) ? 1u : 0u;
     // ---- find or insert the key's slot (lookup phase, then claim phase)
     int32_t slot = -1;
     bool need = live, failed = false;
-    const uint32_t home = (uint32_t)q.h & (NS - 1);
+    const uint32_t home = slot_home(q.h);
     if (a.ablate & kAblNoProbe) { if (need) slot = (int32_t)home; need = false; }
     for (;;) {
         if (!__any(need)) break;
         uint32_t cand = kNone;
         if (need) {
+            // linear probing from a 4-aligned home, one 4-slot bucket per step: the key
+            // is in the chain before its first free slot (nothing is deleted mid-batch)
             uint32_t p = home;
-            for (uint32_t step = 0; step < NS; ++step) {
-                const uint32_t o = s_occ[p];
-                const uint64_t tg = s_tag[p];
-                if ((o & 1u) == 0u) { cand = p; break; }
-                if (tg == q.h) { slot = (int32_t)p; need = false; break; }
-                p = (p + 1) & (NS - 1);
+            for (uint32_t step = 0; step < NS / 4; ++step) {
+                const uint4 o4 = *(const uint4*)&S.occ[p];
+                const ulonglong2 t01 = *(const ulonglong2*)&S.tag[p];
+                const ulonglong2 t23 = *(const ulonglong2*)&S.tag[p + 2];
+                const uint32_t occm = (o4.x & 1u) | (o4.y & 1u) << 1 | (o4.z & 1u) << 2 |
+                                      (o4.w & 1u) << 3;
+                const uint32_t hit = occm & ((t01.x == q.h ? 1u : 0u) | (t01.y == q.h ? 2u : 0u) |
+                                             (t23.x == q.h ? 4u : 0u) | (t23.y == q.h ? 8u : 0u));
+                const uint32_t freem = ~occm & 15u;
+                // first free slot vs first hit in scan order
+                const uint32_t ff = freem ? (uint32_t)__builtin_ctz(freem) : 4u;
+                const uint32_t fh = hit ? (uint32_t)__builtin_ctz(hit) : 4u;
+                if (fh < ff) { slot = (int32_t)(p + fh); need = false; break; }
+                if (ff < 4u) { cand = p + ff; break; }
+                p = (p + 4) & (NS - 1);
             }
             if (need && cand == kNone) { need = false; failed = true; }
         }
         wave_fence();
-        if (need && atomicCAS(&s_occ[cand], 0u, 1u) == 0u) {
-            s_tag[cand] = q.h; s_a[cand] = 0; s_b[cand] = 0; s_c[cand] = 0;
+        if (need && atomicCAS(&S.occ[cand], 0u, 1u) == 0u) {
+            S.tag[cand] = q.h; S.sa[cand] = 0; S.sb[cand] = 0; S.sc[cand] = 0;
             slot = (int32_t)cand;
             need = false;
         }
         wave_fence();
     }
     if (failed) {
-        out = pack_result(false, kRemError);
+        r.out = pack_result(false, kRemError);
         ++n_caperr;
     }
-    if (slot >= 0) atomicOr(&s_occ[slot], 2u);
+    if (slot >= 0) atomicOr(&S.occ[slot], 2u);
     // ---- apply in arrival order: per round, the first state-changing request of each
     // key applies; the key's earlier (non-mutating) requests are final.
     const bool one_round = (a.ablate & kAblNoRounds) != 0;
@@ -426,120 +445,157 @@ __device__ inline void wave_apply(const RegionArgs& a, BinLds<Codec>& S, const D
         if (pending) {
             if (a.ablate & kAblNoStep) {
                 o.mutate = (q.permits & 1) != 0; o.allowed = o.mutate; o.remaining = q.permits;
-                o.a = s_a[slot]; o.b = s_b[slot]; o.c = s_c[slot];
+                o.a = S.sa[slot]; o.b = S.sb[slot]; o.c = S.sc[slot];
             } else {
-                o = tb ? tb_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot])
-                       : sw_step(L, q.op, q.permits, q.now_ms, s_a[slot], s_b[slot], s_c[slot]);
+                o = tb ? tb_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot])
+                       : sw_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot]);
             }
         }
         const uint64_t mut = __ballot(pending && o.mutate) & peers;
         const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
         if (pending && lane <= fm) {
-            if (lane == fm) { s_a[slot] = o.a; s_b[slot] = o.b; s_c[slot] = o.c; }
-            out = pack_result(o.allowed, o.remaining);
-            otok = o.tokens;
+            if (lane == fm) { S.sa[slot] = o.a; S.sb[slot] = o.b; S.sc[slot] = o.c; }
+            r.out = pack_result(o.allowed, o.remaining);
+            r.tok = o.tokens;
             n_allowed += o.allowed ? 1u : 0u;
             pending = false;
         }
         wave_fence();
     }
-    ((Res*)a.res)[j] = (Res)out;
-    if (TOK) a.tok[j] = otok;
+    return r;
 }
 
-template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(kBinThreads) void k_bin(RegionArgs a) {
+template <class Codec, class Res, bool TOK, int BS>
+__global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
-    __shared__ BinLds<Codec> S;
+    constexpr uint32_t RPB = 1u << BS;              // regions per bin
+    __shared__ RegionLds<Codec, (RPB > 1)> S;
 
-    const uint32_t bin = blockIdx.x;
+    // RPB = 8: block g = 64q + 8r + x  ->  bin 8q + x, region r of that bin (see above)
+    const uint32_t g = blockIdx.x;
+    const uint32_t bin = RPB == 1 ? g : (g / 64) * 8 + (g % 8);
+    const uint32_t rb = RPB == 1 ? 0u : (g / 8) % 8;
+    const uint32_t n_bins = a.n_regions / RPB;
+    if (bin >= n_bins) return;
     const uint32_t cnt = a.rcount[bin];
     if (cnt == 0) return;
     const uint32_t start = a.rstart[bin];
     const uint32_t end = start + cnt;
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint32_t region = bin * kRegionsPerBin + w;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t region = bin * RPB + rb;
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
     const int64_t batch_min = (int64_t)(a.ctl->min_now_key ^ 0x8000000000000000ULL);
     const uint32_t pad = a.n_total + lane;          // padding slot for idle lanes
     const Rec* recs = (const Rec*)a.rec;
+    Res* res = (Res*)a.res;
 
     if (a.ctl->span_overflow != 0) {
         // compact records cannot represent this batch's time span: reject it whole,
-        // before any state is touched (the host reports RL_E_INVALID_ARG).
-        for (uint32_t j = start + t; j < end; j += kBinThreads) {
-            ((Res*)a.res)[j] = (Res)pack_result(false, kRemInvalid);
-            if (TOK) a.tok[j] = __builtin_nan("");
+        // before any state is touched (the host reports RL_E_INVALID_ARG). Wave rb of
+        // the bin writes its region's share.
+        for (uint32_t j = start + lane; j < end; j += 64) {
+            const Rec r = recs[j];
+            if ((region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb) {
+                res[j] = (Res)pack_result(false, kRemInvalid);
+                if (TOK) a.tok[j] = __builtin_nan("");
+            }
         }
         return;
     }
-    Rec nxt = recs[min(start + t, end - 1)];        // first chunk, in flight during the load
+    // kDepth slices of the bin's stream in flight (issued while the region image loads)
+    constexpr uint32_t kDepth = 4;
+    auto fetch = [&](uint32_t c) { return recs[min(c + lane, end - 1)]; };  // unconditional
+    Rec q0 = fetch(start), q1 = fetch(start + 64), q2 = fetch(start + 128), q3 = fetch(start + 192);
 
-    // ---- load this wave's region, dropping entries no request of this batch can see,
-    // and rebuild its open-addressing table (no tombstones ever reach HBM)
+    // ---- load the region, dropping entries no request of this batch can see, and
+    // rebuild its open-addressing table (no tombstones ever reach HBM)
     Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
-    for (uint32_t s = lane; s < NS; s += 64) S.occ[w][s] = 0;
-    if (t < 4) S.stat[t] = 0;
+    Slot img[NS / 64];
+#pragma unroll
+    for (uint32_t i = 0; i < NS / 64; ++i) {
+        S.occ[lane + 64 * i] = 0;
+        img[i] = tab[lane + 64 * i];
+    }
     wave_fence();
-    for (uint32_t s = lane; s < NS; s += 64) {
-        const Slot v = tab[s];
+#pragma unroll
+    for (uint32_t i = 0; i < NS / 64; ++i) {
+        const Slot v = img[i];
         if (slot_live(L, v, batch_min)) {
-            uint32_t p = (uint32_t)v.tag & (NS - 1);
-            while (atomicCAS(&S.occ[w][p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
-            S.tag[w][p] = v.tag; S.sa[w][p] = v.a; S.sb[w][p] = v.b; S.sc[w][p] = v.c;
+            uint32_t p = slot_home(v.tag);
+            while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+            S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
         }
     }
     wave_fence();
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0;
-    uint32_t head = 0, count = 0;                    // this wave's ring (wave-uniform)
-    for (uint32_t c0 = start; c0 < end; c0 += kChunk) {
-        const uint32_t m = min((uint32_t)kChunk, end - c0);
-        __syncthreads();                             // every wave is done with `stage`
-        S.stage[t] = nxt;
-        nxt = recs[min(c0 + kChunk + t, end - 1)];
-        __syncthreads();
-        // each wave takes its region's requests out of the chunk, in arrival order, and
-        // applies them 64 at a time
-        for (uint32_t sl = 0; sl < (uint32_t)kChunk / 64; ++sl) {
-            const uint32_t idx = sl * 64 + lane;
-            if (sl * 64 >= m) break;
-            const bool v = idx < m;
-            const Rec r = S.stage[idx];
-            const uint32_t lim = Codec::limiter_of(r);
-            const DevLimiter& LL = L;
-            (void)lim;
-            const uint32_t reg = LL.region_base +
-                                 region_local(r.h, a.shard_bits, LL.region_bits);
-            const bool mine = v && (reg & (kRegionsPerBin - 1)) == w;
+    uint32_t head = 0, count = 0;                    // ring state (wave-uniform)
+    auto slice = [&](const Rec& r, uint32_t c0) {
+        const uint32_t idx = c0 + lane;
+        if constexpr (RPB == 1) {
+            // the bin is the region: every record is ours, applied straight from registers
+            const Applied ap = wave_apply<Codec>(a, S, L, lane, r, idx < end, idx, base, pad,
+                                                 n_allowed, n_invalid, n_caperr);
+            res[ap.j] = (Res)ap.out;
+            if (TOK) a.tok[ap.j] = ap.tok;
+        } else {
+            const bool mine = idx < end &&
+                (region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb;
             const uint64_t bal = __ballot(mine);
             if (mine) {
                 const uint32_t k = (head + count + popc_below(bal)) % kRing;
-                S.ring[w][k] = r;
-                S.ring_pos[w][k] = c0 + idx;
+                S.ring[k] = r;
+                S.ring_pos[k] = idx;
             }
             count += (uint32_t)__popcll(bal);
             wave_fence();
+            Applied ap;
+            ap.j = pad; ap.out = 0; ap.tok = 0.0;
             if (count >= 64) {
-                wave_apply<Codec, Res, TOK>(a, S, L, w, lane, head, 64, base, pad, n_allowed,
-                                            n_invalid, n_caperr);
+                const uint32_t ri = (head + lane) % kRing;
+                ap = wave_apply<Codec>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
+                                       n_allowed, n_invalid, n_caperr);
                 head = (head + 64) % kRing;
                 count -= 64;
             }
+            res[ap.j] = (Res)ap.out;                 // exactly one store per slice
+            if (TOK) a.tok[ap.j] = ap.tok;
+        }
+    };
+    // unrolled by kDepth so the prefetch registers rotate without moves (a register move
+    // would wait on its load and shrink the effective depth to one slice)
+    for (uint32_t c0 = start; c0 < end; c0 += 64 * kDepth) {
+        slice(q0, c0);
+        q0 = fetch(c0 + 64 * kDepth);
+        if (c0 + 64 >= end) break;
+        slice(q1, c0 + 64);
+        q1 = fetch(c0 + 64 * kDepth + 64);
+        if (c0 + 128 >= end) break;
+        slice(q2, c0 + 128);
+        q2 = fetch(c0 + 64 * kDepth + 128);
+        if (c0 + 192 >= end) break;
+        slice(q3, c0 + 192);
+        q3 = fetch(c0 + 64 * kDepth + 192);
+    }
+    if constexpr (RPB > 1) {
+        if (count > 0) {
+            const bool v = lane < count;
+            const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
+            const Applied ap = wave_apply<Codec>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
+                                                 pad, n_allowed, n_invalid, n_caperr);
+            res[ap.j] = (Res)ap.out;
+            if (TOK) a.tok[ap.j] = ap.tok;
         }
     }
-    if (count > 0)
-        wave_apply<Codec, Res, TOK>(a, S, L, w, lane, head, count, base, pad, n_allowed,
-                                    n_invalid, n_caperr);
     wave_fence();
     // ---- write the region back (free slots as zeros)
     uint32_t touched = 0;
     for (uint32_t s = lane; s < NS; s += 64) {
-        const uint32_t o = S.occ[w][s];
+        const uint32_t o = S.occ[s];
         Slot v;
-        if (o & 1u) { v.tag = S.tag[w][s]; v.a = S.sa[w][s]; v.b = S.sb[w][s]; v.c = S.sc[w][s]; }
+        if (o & 1u) { v.tag = S.tag[s]; v.a = S.sa[s]; v.b = S.sb[s]; v.c = S.sc[s]; }
         else { v.tag = 0; v.a = 0; v.b = 0; v.c = 0; }
         tab[s] = v;
         touched += (o >> 1) & 1u;
@@ -551,18 +607,11 @@ __global__ __launch_bounds__(kBinThreads) void k_bin(RegionArgs a) {
         touched += __shfl_xor(touched, off, 64);
     }
     if (lane == 0) {
-        atomicAdd(&S.stat[0], n_allowed);
-        atomicAdd(&S.stat[1], n_invalid);
-        atomicAdd(&S.stat[2], n_caperr);
-        atomicAdd(&S.stat[3], touched);
-    }
-    __syncthreads();
-    if (t == 0) {
-        atomicAdd(&a.ctl->allowed, (unsigned long long)S.stat[0]);
-        if (S.stat[1]) atomicAdd(&a.ctl->invalid, (unsigned long long)S.stat[1]);
-        if (S.stat[2]) atomicAdd(&a.ctl->cap_err, (unsigned long long)S.stat[2]);
-        atomicAdd(&a.ctl->distinct, (unsigned long long)S.stat[3]);
-        atomicAdd(&a.ctl->regions, (unsigned long long)kRegionsPerBin);
+        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
+        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
+        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
+        atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
+        atomicAdd(&a.ctl->regions, 1ULL);
     }
 }
 
@@ -822,9 +871,17 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
 
 template <class Codec, class Res>
 static void region_launch(const RegionArgs& a, hipStream_t s) {
-    const dim3 g(a.n_regions / kRegionsPerBin), b(kBinThreads);
-    if (a.tok) hipLaunchKernelGGL((k_bin<Codec, Res, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((k_bin<Codec, Res, false>), g, b, 0, s, a);
+    const dim3 b(64);
+    if (a.bin_shift == 0) {
+        const dim3 g(a.n_regions);
+        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0>), g, b, 0, s, a);
+    } else {
+        const uint32_t n_bins = a.n_regions / kRegionsPerBin;
+        const dim3 g((n_bins + 7) / 8 * 64);
+        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 3>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 3>), g, b, 0, s, a);
+    }
 }
 
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {

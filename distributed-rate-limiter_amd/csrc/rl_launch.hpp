@@ -52,6 +52,7 @@ struct PartArgs {
     const DevLimiter* lims;
     int32_t digit_shift;
     int32_t digit_bits;
+    int32_t bin_shift;         // bin = region >> bin_shift (0: one region per bin, 3: eight)
     uint32_t* counts;          // [bins][n_tiles]: per-tile histogram, then exclusive row scan
     const uint32_t* bin_base;  // [bins]
     uint32_t* region_count;    // nullable: full-region histogram (multi-pass only)
@@ -71,6 +72,7 @@ struct RegionArgs {
     uint32_t n_regions;        // multiple of kRegionsPerBin; one workgroup per bin
     uint32_t n_total;          // batch size: res/tok carry 64 padding entries past it
     int32_t shard_bits;
+    int32_t bin_shift;
     uint32_t ablate;
 };
 

@@ -18,7 +18,8 @@ from bench import CONFIGS, NS, T0_NS  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="tb_uniform")
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="0,1,2,4,8,16,20,256,512,1024,1536,65536")
+ap.add_argument("--variants", default="ablate=0/ablate=256/ablate=512/ablate=1024",
+                help="'/'-separated variants, each a ','-separated list of rl_tune key=value")
 args = ap.parse_args()
 cfg = CONFIGS[args.config]
 n = cfg["batch"]
@@ -35,15 +36,25 @@ eng.synth_trace(n, keys, permits, now, None, seed=cfg["seed"], n_keys=cfg["n_key
                 t0_ns=T0_NS, span_ns=cfg["span_ns"], n_total=n)
 allowed = torch.empty(n, dtype=torch.uint8, device=dev)
 remaining = torch.empty(n, dtype=torch.int64, device=dev)
-variants = [int(v) for v in args.variants.split(",")]
+variants = args.variants.split("/")
+
+
+def apply(v):
+    eng.tune("ablate", 0)
+    for kv in v.split(","):
+        k, x = kv.split("=")
+        eng.tune(k, int(x))
+
+
+
 res = {v: {} for v in variants}
 for v in variants:                                  # warm every variant once
-    eng.tune("ablate", v)
+    apply(v)
     eng.execute_device(n, keys, permits, now, None, None, allowed, remaining)
 eng.stage_times()
 for r in range(args.rounds):
     for v in variants:
-        eng.tune("ablate", v)
+        apply(v)
         eng.execute_device(n, keys, permits, now, None, None, allowed, remaining)
         st = eng.stage_times()
         for k, ms in st.items():
