@@ -106,6 +106,7 @@ struct rl_engine {
     uint64_t last_n = 0;
     uint32_t ablate = 0;                    // rl_tune("ablate"), measurement only
     int bin_shift = 0;                      // rl_tune("bin_shift"): 0 or 3 (regions per bin 1/8)
+    uint32_t up_per_cu = 0, sc_per_cu = 0, un_per_cu = 0;   // rl_tune("*_per_cu"), 0 = default
 };
 
 #define HIP_OK(x)                                                      \
@@ -386,6 +387,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = e->d_ctl;
     pa.counts = e->counts; pa.bin_base = e->bin_base; pa.ablate = e->ablate;
     pa.bin_shift = bsh;
+    pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu;
     // ---- pass 0 (low digit) from the caller's arrays
     pa.digit_shift = 0; pa.digit_bits = d0;
     pa.region_count = nullptr;
@@ -442,7 +444,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
     ua.tok = tokens_after ? e->tok : nullptr;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
-    ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate;
+    ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate; ua.per_cu = e->un_per_cu;
     HIP_OK(launch_unpermute(ua, res_bytes, s));
     mark(e, 9);
     if (e->timing) {
@@ -621,6 +623,9 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (!e || !key) return RL_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(e->mu);
     if (std::strcmp(key, "ablate") == 0) { e->ablate = (uint32_t)value; return RL_OK; }
+    if (std::strcmp(key, "upsweep_per_cu") == 0) { e->up_per_cu = (uint32_t)value; return RL_OK; }
+    if (std::strcmp(key, "scatter_per_cu") == 0) { e->sc_per_cu = (uint32_t)value; return RL_OK; }
+    if (std::strcmp(key, "unpermute_per_cu") == 0) { e->un_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "bin_shift") == 0) {
         if (value != 0 && value != kBinShift) return RL_E_INVALID_ARG;
         e->bin_shift = (int)value;

@@ -229,6 +229,8 @@ struct ScatterIn<Codec, false> {
     }
 };
 
+constexpr int kScatterDepth = 8;        // rounds of inputs in flight (divides kTileItems)
+
 template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     using Rec = typename Codec::Rec;
@@ -254,19 +256,15 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
 #pragma unroll
             for (int w = 0; w < kTileThreads / 64; ++w) cntw[w][b] = 0;
         }
-        // two rounds of inputs in flight; out-of-range lanes re-load element n-1 so every
-        // wave issues the same loads and stores each round (static vmcnt counting: the
-        // waits for round r+2's inputs never include round r's scattered stores).
-        ScatterIn<Codec, RAW> nx1, nx2;
-        nx1.load(a, min(tile0 + t, last));
-        nx2.load(a, min(tile0 + kTileThreads + t, last));
+        // kScatterDepth rounds of inputs in flight; out-of-range lanes re-load element n-1
+        // so every wave issues the same loads and stores each round (static vmcnt counting)
+        ScatterIn<Codec, RAW> in[kScatterDepth];
+#pragma unroll
+        for (int k = 0; k < kScatterDepth; ++k) in[k].load(a, min(tile0 + (uint32_t)k * kTileThreads + t, last));
         __syncthreads();
-        for (int r = 0; r < kTileItems; ++r) {
+        auto round = [&](const ScatterIn<Codec, RAW>& in, int r) {
             const uint32_t i = tile0 + (uint32_t)r * kTileThreads + t;
             const bool active = i < a.n;
-            const ScatterIn<Codec, RAW> in = nx1;
-            nx1 = nx2;
-            nx2.load(a, min(i + 2 * kTileThreads, last));
             Rec rec{};
             uint32_t d = 0;
             if (active) {
@@ -317,6 +315,17 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
             if (abl & kAblSeqRecStore) wpos = active ? i : a.n + t;
             if (!(abl & kAblNoRecStore)) ((Rec*)a.rec_out)[wpos] = rec;
             if (!(abl & kAblNoPosStore)) a.pos_out[active ? i : a.n + t] = pos;
+        };
+        // Unrolled by the prefetch depth so the input registers rotate without moves (a
+        // move would wait on its load). vmcnt retires loads and stores in issue order, so
+        // waiting for round r's inputs also waits for the scattered stores issued before
+        // them: a deep ring spreads that store-ack latency over kScatterDepth rounds.
+        for (int r = 0; r < kTileItems; r += kScatterDepth) {
+#pragma unroll
+            for (int k = 0; k < kScatterDepth; ++k) {
+                round(in[k], r + k);
+                in[k].load(a, min(tile0 + (uint32_t)(r + k + kScatterDepth) * kTileThreads + t, last));
+            }
         }
     }
     if constexpr (RAW) {
@@ -377,13 +386,13 @@ struct Applied {
 };
 
 // Apply one group of up to 64 requests (lane order = arrival order; `valid` lanes only).
-template <class Codec, class LdsT>
+template <class Codec, int ALGO, class LdsT>
 __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimiter& L,
                                      uint32_t lane, const typename Codec::Rec& cur, bool valid,
                                      uint32_t j, int64_t base, uint32_t pad, uint32_t& n_allowed,
                                      uint32_t& n_invalid, uint32_t& n_caperr) {
     constexpr uint32_t NS = kRegionSlots;
-    const bool tb = L.algo == kAlgoTB;
+    constexpr bool tb = ALGO == kAlgoTB;        // per-algorithm code: nothing of the other
     Applied r;
     r.j = valid ? j : pad;
     const Req q = Codec::dec(cur, base);
@@ -447,8 +456,10 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 o.mutate = (q.permits & 1) != 0; o.allowed = o.mutate; o.remaining = q.permits;
                 o.a = S.sa[slot]; o.b = S.sb[slot]; o.c = S.sc[slot];
             } else {
-                o = tb ? tb_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot])
-                       : sw_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot]);
+                if constexpr (tb)
+                    o = tb_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot]);
+                else
+                    o = sw_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot]);
             }
         }
         const uint64_t mut = __ballot(pending && o.mutate) & peers;
@@ -532,63 +543,70 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0;
     uint32_t head = 0, count = 0;                    // ring state (wave-uniform)
-    auto slice = [&](const Rec& r, uint32_t c0) {
-        const uint32_t idx = c0 + lane;
-        if constexpr (RPB == 1) {
-            // the bin is the region: every record is ours, applied straight from registers
-            const Applied ap = wave_apply<Codec>(a, S, L, lane, r, idx < end, idx, base, pad,
-                                                 n_allowed, n_invalid, n_caperr);
-            res[ap.j] = (Res)ap.out;
-            if (TOK) a.tok[ap.j] = ap.tok;
-        } else {
-            const bool mine = idx < end &&
-                (region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb;
-            const uint64_t bal = __ballot(mine);
-            if (mine) {
-                const uint32_t k = (head + count + popc_below(bal)) % kRing;
-                S.ring[k] = r;
-                S.ring_pos[k] = idx;
+    // the whole stream is instantiated once per algorithm (uniform per region), so the
+    // compiler hoists nothing of the other algorithm into the hot loop
+    auto stream = [&](auto algo) {
+        constexpr int A = decltype(algo)::value;
+        auto slice = [&](const Rec& r, uint32_t c0) {
+            const uint32_t idx = c0 + lane;
+            if constexpr (RPB == 1) {
+                // the bin is the region: every record is ours, applied straight from registers
+                const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, idx < end, idx, base, pad,
+                                                     n_allowed, n_invalid, n_caperr);
+                res[ap.j] = (Res)ap.out;
+                if (TOK) a.tok[ap.j] = ap.tok;
+            } else {
+                const bool mine = idx < end &&
+                    (region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb;
+                const uint64_t bal = __ballot(mine);
+                if (mine) {
+                    const uint32_t k = (head + count + popc_below(bal)) % kRing;
+                    S.ring[k] = r;
+                    S.ring_pos[k] = idx;
+                }
+                count += (uint32_t)__popcll(bal);
+                wave_fence();
+                Applied ap;
+                ap.j = pad; ap.out = 0; ap.tok = 0.0;
+                if (count >= 64) {
+                    const uint32_t ri = (head + lane) % kRing;
+                    ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
+                                           n_allowed, n_invalid, n_caperr);
+                    head = (head + 64) % kRing;
+                    count -= 64;
+                }
+                res[ap.j] = (Res)ap.out;                 // exactly one store per slice
+                if (TOK) a.tok[ap.j] = ap.tok;
             }
-            count += (uint32_t)__popcll(bal);
-            wave_fence();
-            Applied ap;
-            ap.j = pad; ap.out = 0; ap.tok = 0.0;
-            if (count >= 64) {
-                const uint32_t ri = (head + lane) % kRing;
-                ap = wave_apply<Codec>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
-                                       n_allowed, n_invalid, n_caperr);
-                head = (head + 64) % kRing;
-                count -= 64;
+        };
+        // unrolled by kDepth so the prefetch registers rotate without moves (a register move
+        // would wait on its load and shrink the effective depth to one slice)
+        for (uint32_t c0 = start; c0 < end; c0 += 64 * kDepth) {
+            slice(q0, c0);
+            q0 = fetch(c0 + 64 * kDepth);
+            if (c0 + 64 >= end) break;
+            slice(q1, c0 + 64);
+            q1 = fetch(c0 + 64 * kDepth + 64);
+            if (c0 + 128 >= end) break;
+            slice(q2, c0 + 128);
+            q2 = fetch(c0 + 64 * kDepth + 128);
+            if (c0 + 192 >= end) break;
+            slice(q3, c0 + 192);
+            q3 = fetch(c0 + 64 * kDepth + 192);
+        }
+        if constexpr (RPB > 1) {
+            if (count > 0) {
+                const bool v = lane < count;
+                const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
+                const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
+                                                     pad, n_allowed, n_invalid, n_caperr);
+                res[ap.j] = (Res)ap.out;
+                if (TOK) a.tok[ap.j] = ap.tok;
             }
-            res[ap.j] = (Res)ap.out;                 // exactly one store per slice
-            if (TOK) a.tok[ap.j] = ap.tok;
         }
     };
-    // unrolled by kDepth so the prefetch registers rotate without moves (a register move
-    // would wait on its load and shrink the effective depth to one slice)
-    for (uint32_t c0 = start; c0 < end; c0 += 64 * kDepth) {
-        slice(q0, c0);
-        q0 = fetch(c0 + 64 * kDepth);
-        if (c0 + 64 >= end) break;
-        slice(q1, c0 + 64);
-        q1 = fetch(c0 + 64 * kDepth + 64);
-        if (c0 + 128 >= end) break;
-        slice(q2, c0 + 128);
-        q2 = fetch(c0 + 64 * kDepth + 128);
-        if (c0 + 192 >= end) break;
-        slice(q3, c0 + 192);
-        q3 = fetch(c0 + 64 * kDepth + 192);
-    }
-    if constexpr (RPB > 1) {
-        if (count > 0) {
-            const bool v = lane < count;
-            const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
-            const Applied ap = wave_apply<Codec>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
-                                                 pad, n_allowed, n_invalid, n_caperr);
-            res[ap.j] = (Res)ap.out;
-            if (TOK) a.tok[ap.j] = ap.tok;
-        }
-    }
+    if (L.algo == kAlgoTB) stream(std::integral_constant<int, kAlgoTB>{});
+    else stream(std::integral_constant<int, kAlgoSW>{});
     wave_fence();
     // ---- write the region back (free slots as zeros)
     uint32_t touched = 0;
@@ -619,15 +637,52 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
 template <class Res>
 __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
   const uint32_t t = threadIdx.x;
+  const Res* __restrict__ res = (const Res*)a.res;
+  const uint32_t* __restrict__ pos0 = a.pos0;
+  const uint32_t* __restrict__ pos1 = a.pos1;
+  uint8_t* __restrict__ allowed = a.allowed;
+  int64_t* __restrict__ remaining = a.remaining;
+  constexpr int B = 8;                         // rounds per batch (loads issued together)
+  constexpr int NB = kTileItems / B;
+  const bool simple = pos1 || a.tokens_out || (a.ablate & kAblNoGather);
   for (uint32_t it = 0;; ++it) {
     const uint32_t tile = tile_at(it);
     if (tile >= a.n_tiles) break;
-    const Res* __restrict__ res = (const Res*)a.res;
-    const uint32_t* __restrict__ pos0 = a.pos0;
-    const uint32_t* __restrict__ pos1 = a.pos1;
-    uint8_t* __restrict__ allowed = a.allowed;
-    int64_t* __restrict__ remaining = a.remaining;
-    constexpr int B = 8;                       // rounds whose loads are issued together
+    const uint32_t tbase = tile * (uint32_t)kTile + t;
+    if (!simple && tile * (uint64_t)kTile + kTile <= a.n) {
+        // Full tile, one result array: software-pipelined so that every wait is for loads
+        // issued a batch earlier and never directly behind the previous batch's stores
+        // (vmcnt retires loads and stores in issue order).
+        uint32_t pE[B], pO[B];
+        Res vE[B], vO[B];
+        auto load = [&](uint32_t (&p)[B], int b) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) p[k] = pos0[tbase + (uint32_t)(b * B + k) * kTileThreads];
+        };
+        auto gather = [&](Res (&v)[B], const uint32_t (&p)[B]) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+        };
+        auto store = [&](const Res (&v)[B], int b) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) {
+                const uint32_t i = tbase + (uint32_t)(b * B + k) * kTileThreads;
+                allowed[i] = (uint8_t)(v[k] & 1u);
+                remaining[i] = (int64_t)(v[k] >> 1) - kResBias;
+            }
+        };
+        load(pE, 0);
+        for (int b = 0; b < NB; b += 2) {
+            gather(vE, pE);
+            load(pO, b + 1);
+            if (b > 0) store(vO, b - 1);
+            gather(vO, pO);
+            load(pE, (b + 2) % NB);                 // unconditional (last one unused)
+            store(vE, b);
+        }
+        store(vO, NB - 1);
+        continue;
+    }
     for (int r0 = 0; r0 < kTileItems; r0 += B) {
         uint32_t p[B];
         Res v[B];
@@ -829,7 +884,7 @@ static uint32_t persistent_grid(uint32_t n_tiles, uint32_t per_cu) {
 }
 
 hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
-    dim3 grid(persistent_grid(a.n_tiles, 2)), block(kTileThreads);
+    dim3 grid(persistent_grid(a.n_tiles, a.up_per_cu ? a.up_per_cu : 4)), block(kTileThreads);
     if (raw) {
         if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_upsweep<CodecC, true>), grid, block, 0, s, a);
@@ -841,7 +896,7 @@ hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s)
 }
 
 hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
-    dim3 grid(persistent_grid(a.n_tiles, 1)), block(kTileThreads);
+    dim3 grid(persistent_grid(a.n_tiles, a.sc_per_cu ? a.sc_per_cu : 1)), block(kTileThreads);
     if (raw) {
         if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, 0, s, a);
@@ -893,7 +948,7 @@ hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStrea
 }
 
 hipError_t launch_unpermute(const UnpermArgs& a, int res_bytes, hipStream_t s) {
-    dim3 g(persistent_grid(a.n_tiles, 1)), b(kTileThreads);
+    dim3 g(persistent_grid(a.n_tiles, a.per_cu ? a.per_cu : 1)), b(kTileThreads);
     if (res_bytes == 8) hipLaunchKernelGGL(k_unpermute<uint64_t>, g, b, 0, s, a);
     else if (res_bytes == 1) hipLaunchKernelGGL(k_unpermute<uint8_t>, g, b, 0, s, a);
     else if (res_bytes == 2) hipLaunchKernelGGL(k_unpermute<uint16_t>, g, b, 0, s, a);

@@ -53,6 +53,8 @@ struct PartArgs {
     int32_t digit_shift;
     int32_t digit_bits;
     int32_t bin_shift;         // bin = region >> bin_shift (0: one region per bin, 3: eight)
+    uint32_t up_per_cu;        // persistent-grid workgroups per CU (0: default)
+    uint32_t sc_per_cu;
     uint32_t* counts;          // [bins][n_tiles]: per-tile histogram, then exclusive row scan
     const uint32_t* bin_base;  // [bins]
     uint32_t* region_count;    // nullable: full-region histogram (multi-pass only)
@@ -87,6 +89,7 @@ struct UnpermArgs {
     uint32_t n;
     uint32_t n_tiles;
     uint32_t ablate;
+    uint32_t per_cu;           // persistent-grid workgroups per CU (0: default)
 };
 
 struct SynthArgs {

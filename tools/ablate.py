@@ -39,8 +39,13 @@ remaining = torch.empty(n, dtype=torch.int64, device=dev)
 variants = args.variants.split("/")
 
 
+DEFAULTS = {"ablate": 0, "bin_shift": 0, "upsweep_per_cu": 0, "scatter_per_cu": 0,
+            "unpermute_per_cu": 0}
+
+
 def apply(v):
-    eng.tune("ablate", 0)
+    for k, x in DEFAULTS.items():          # every variant starts from the defaults
+        eng.tune(k, x)
     for kv in v.split(","):
         k, x = kv.split("=")
         eng.tune(k, int(x))
