@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Fold a tools/profile.sh output directory into profiles/pmc_summary.json, the file
+bench.py reads `roofline.traffic` from.
+
+Per pipeline stage (bench.py's stage names) it records the rocprofv3 kernel-trace
+average duration and the per-launch HBM-side byte counters, corrected as
+/opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes:
+  * FETCH_SIZE / WRITE_SIZE are reported in KiB            -> x 1024
+  * FETCH_SIZE counts half the bytes of wide streaming reads on gfx950 -> x 2
+  * WRITE_SIZE is exact for streaming stores               -> x 1
+Both counters are taken from their own --pmc pass (they do not fit one pass). They
+count L2 -> fabric traffic, so Infinity-Cache hits are included: the figure is an
+upper bound on HBM bytes.
+
+usage: tools/pmc_json.py <profile dir> <config name> [--out profiles/pmc_summary.json]
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+
+
+def stage_of(name: str):
+    if "k_upsweep<" in name:
+        return "upsweep0" if name.rstrip(")").split(">")[0].endswith("true") else "upsweep1"
+    if "k_scatter<" in name:
+        return "scatter0" if name.rstrip(")").split(">")[0].endswith("true") else "scatter1"
+    if "k_regions<" in name:
+        return "region"
+    if "k_unpermute<" in name:
+        return "unpermute"
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("config")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "profiles", "pmc_summary.json"))
+    ap.add_argument("--tag", default="")
+    a = ap.parse_args()
+    base = a.prof_dir.rstrip("/")
+    st = {}
+    for r in csv.DictReader(open(f"{base}/trace/trace_kernel_stats.csv")):
+        s = stage_of(r["Name"])
+        if s:
+            st[s] = {"kernel": r["Name"], "calls": int(r["Calls"]),
+                     "avg_us": float(r["AverageNs"]) / 1e3}
+    counters = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in ("fetch", "write", "tcc", "sq"):
+        p = f"{base}/{f}/{f}_counter_collection.csv"
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            s = stage_of(r["Kernel_Name"])
+            if s:
+                counters[s][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for s, cs in counters.items():
+        d = st.setdefault(s, {})
+        mean = {k: sum(v) / len(v) for k, v in cs.items()}
+        if "FETCH_SIZE" in mean:
+            d["fetch_kib_raw"] = mean["FETCH_SIZE"]
+            d["fetch_bytes"] = mean["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in mean:
+            d["write_bytes"] = mean["WRITE_SIZE"] * 1024
+        if "fetch_bytes" in d and "write_bytes" in d:
+            d["hbm_bytes_per_launch"] = d["fetch_bytes"] + d["write_bytes"]
+        if "TCC_HIT_sum" in mean and "TCC_MISS_sum" in mean:
+            tot = mean["TCC_HIT_sum"] + mean["TCC_MISS_sum"]
+            d["l2_hit_rate"] = mean["TCC_HIT_sum"] / tot if tot else None
+        for k in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY",
+                  "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES"):
+            if k in mean:
+                d[k] = mean[k]
+    out = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    out[a.config] = st
+    out.setdefault("_meta", {})["note"] = (
+        "per-launch means; fetch_bytes = FETCH_SIZE KiB x1024 x2 (gfx950 wide-read "
+        "correction), write_bytes = WRITE_SIZE KiB x1024; L2->fabric bytes, Infinity-Cache "
+        "hits included (upper bound on HBM bytes)")
+    if a.tag:
+        out["_meta"][a.config] = a.tag
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
+    for s, d in sorted(st.items()):
+        print(f"{s:10s} {d.get('avg_us', 0):9.1f} us  hbm/launch "
+              f"{d.get('hbm_bytes_per_launch', 0) / 1e9:.3f} GB  l2hit {d.get('l2_hit_rate') or 0:.2f}")
+
+
+if __name__ == "__main__":
+    main()
