@@ -199,16 +199,30 @@ struct Outcome {
 };
 
 // ---------------------------------------------------------------- token bucket
-// TokenBucketRateLimiter.tryAcquire (:105-143) + Lua (:38-68). `last` is the ms
-// timestamp stored by HMSET; the bucket exists iff written and now <= last + 2w.
+// Lua :46-58: the balance after refill at `now` (absent or expired bucket: full).
+// `last` is the ms timestamp stored by HMSET; the bucket exists iff written and
+// now <= last + 2w. Non-decreasing in `now` for a fixed state (the hot-key fast
+// path relies on that, k_regions_hot).
+__device__ inline double tb_refill(const DevLimiter& L, int64_t now, uint64_t a, uint64_t b,
+                                   uint64_t c) {
+    const int64_t last = (int64_t)b;
+    const bool exists = (c & 1u) && !(now > last + L.ttl_ms);
+    const double capacity = L.capacity;
+    const double nowd = (double)now;
+    const double tokens = exists ? __longlong_as_double((long long)a) : capacity;
+    const double last_refill = exists ? (double)last : nowd;
+    const double elapsed = nowd - last_refill;               // Lua :56
+    const double tokens_to_add = elapsed * L.rate_per_ms;    // Lua :57
+    const double x = tokens + tokens_to_add;                 // Lua :58
+    return x < capacity ? x : capacity;                      // math.min(capacity, x)
+}
+
+// TokenBucketRateLimiter.tryAcquire (:105-143) + Lua (:38-68).
 __device__ inline Outcome tb_step(const DevLimiter& L, uint32_t op, int32_t permits,
                                   int64_t now, uint64_t a, uint64_t b, uint64_t c) {
     Outcome o;
     o.mutate = false; o.allowed = false; o.remaining = 0; o.tokens = __builtin_nan("");
     o.a = a; o.b = b; o.c = c;
-    const int64_t last = (int64_t)b;
-    const bool exists = (c & 1u) && !(now > last + L.ttl_ms);
-    const double capacity = L.capacity;
     if (op == (uint32_t)kOpReset) {                  // DEL tb:key (:153-158)
         o.mutate = true; o.a = 0; o.b = 0; o.c = 0;
         return o;
@@ -217,13 +231,7 @@ __device__ inline Outcome tb_step(const DevLimiter& L, uint32_t op, int32_t perm
         o.remaining = kRemUnknown;
         return o;
     }
-    const double nowd = (double)now;
-    double tokens = exists ? __longlong_as_double((long long)a) : capacity;
-    const double last_refill = exists ? (double)last : nowd;
-    const double elapsed = nowd - last_refill;               // Lua :56
-    const double tokens_to_add = elapsed * L.rate_per_ms;    // Lua :57
-    const double x = tokens + tokens_to_add;                 // Lua :58
-    tokens = x < capacity ? x : capacity;                    // math.min(capacity, x)
+    double tokens = tb_refill(L, now, a, b, c);
     if (op == (uint32_t)kOpPeek) {
         o.remaining = d2l(tokens);
         o.tokens = tokens;

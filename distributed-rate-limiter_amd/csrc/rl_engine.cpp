@@ -23,12 +23,13 @@ namespace {
 
 // Stage timing: events bracket every kernel of a batch; a ring of per-batch event
 // sets is averaged when rl_stage_times is called (no host sync inside a batch).
-constexpr int kMarks = 10;   // marks 0..9
-constexpr int kStages = 10;
+constexpr int kMarks = 12;   // marks 0..9 on the engine stream, 10..11 on the hot stream
+constexpr int kStages = 11;
 const char* kStageNames[kStages] = {"upsweep0", "scan0", "scatter0", "upsweep1", "scan1",
-                                    "scatter1", "region_offsets", "region", "unpermute", "total"};
+                                    "scatter1", "region_offsets", "region", "unpermute", "total",
+                                    "region_hot"};
 const int kStagePairs[kStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6},
-                                     {6, 7}, {7, 8}, {8, 9}, {0, 9}};
+                                     {6, 7}, {7, 8}, {8, 9}, {0, 9}, {10, 11}};
 constexpr int kEvRing = 64;
 
 struct HostLimiter {
@@ -51,6 +52,8 @@ struct rl_engine {
     rl_opts opts{};
     int shard_bits = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream_hot = nullptr;       // k_regions_hot runs beside k_regions
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::mutex mu;                          // one batch in flight per engine handle
 
     std::vector<HostLimiter> lims;
@@ -74,9 +77,19 @@ struct rl_engine {
     uint32_t* bin_base = nullptr;           // [4096]
     uint32_t* region_count = nullptr;       // [P padded]
     uint32_t* region_start = nullptr;
-    uint32_t* row_tmp = nullptr;
-    uint32_t* row_base = nullptr;
     size_t region_cap = 0;
+    // hot regions
+    uint32_t* hot_list = nullptr;           // [kHotMax + 40]: list, k_hot_select's meta, total
+    HotInfo* hot_info = nullptr;            // [kHotMax]
+    uint64_t* hot_summ = nullptr;           // [hot_summ_cap][4]
+    size_t hot_summ_cap = 0;
+    uint32_t* hot_mark = nullptr;           // [hot_mark_cap] epoch marks per bin
+    size_t hot_mark_cap = 0;
+    uint32_t epoch = 0;
+    uint32_t hot_threshold = 16384;         // rl_tune("hot_threshold"); 0 disables
+    uint64_t* dbg = nullptr;                // rl_tune("debug_regions"): per-bin stamps
+    size_t dbg_cap = 0;
+    bool debug_regions = false;
     BatchCtl* d_ctl = nullptr;
     BatchCtl* h_ctl = nullptr;              // pinned copy of the last batch's ctl
 
@@ -163,6 +176,14 @@ extern "C" uint32_t rl_owner_of(uint64_t key_hash, uint16_t, uint32_t shard_coun
     return (uint32_t)(mix64(key_hash) >> (64 - s));
 }
 
+// The hot-region kernel must get its CUs before the (much larger) normal region grid
+// fills the machine, so its stream has the greatest priority the device offers.
+static int hot_priority() {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+    return greatest;
+}
+
 extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     if (!out) return RL_E_INVALID_ARG;
     *out = nullptr;
@@ -184,8 +205,11 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     } else {
         (void)hipGetDevice(&e->device);
     }
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete e;
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&e->stream_hot, hipStreamNonBlocking, hot_priority()) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
+        rl_destroy(e);
         return RL_E_DEVICE;
     }
     e->timing = (o.flags & RL_OPT_STAGE_TIMING) != 0;
@@ -197,6 +221,8 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
     if (rc == RL_OK) rc = dalloc(&e->bin_total, 1u << kMaxDigitBits);
     if (rc == RL_OK) rc = dalloc(&e->bin_base, 1u << kMaxDigitBits);
+    if (rc == RL_OK) rc = dalloc(&e->hot_list, kHotMax + 40);
+    if (rc == RL_OK) rc = dalloc(&e->hot_info, kHotMax);
     if (rc != RL_OK) { rl_destroy(e); return rc; }
     std::memset(e->h_ctl, 0, sizeof(BatchCtl));
     *out = e;
@@ -210,7 +236,8 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->d_lims); dfree(e->d_region_lim);
     dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
     dfree(e->counts); dfree(e->bin_total); dfree(e->bin_base);
-    dfree(e->region_count); dfree(e->region_start); dfree(e->row_tmp); dfree(e->row_base);
+    dfree(e->region_count); dfree(e->region_start);
+    dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
     dfree(e->d_ctl);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
@@ -218,6 +245,9 @@ extern "C" void rl_destroy(rl_engine* e) {
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
     for (int r = 0; r < kEvRing; ++r)
         for (int i = 0; i < kMarks; ++i) if (e->ev[r][i]) (void)hipEventDestroy(e->ev[r][i]);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->stream_hot) { (void)hipStreamSynchronize(e->stream_hot); (void)hipStreamDestroy(e->stream_hot); }
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -322,21 +352,40 @@ static int ensure_scratch(rl_engine* e, size_t n, bool wide, uint32_t bins, uint
     return RL_OK;
 }
 
-static int ensure_regions(rl_engine* e, size_t padded) {
-    if (padded <= e->region_cap) return RL_OK;
-    dfree(e->region_count); dfree(e->region_start); dfree(e->row_tmp); dfree(e->row_base);
-    int rc = dalloc(&e->region_count, padded);
-    if (rc == RL_OK) rc = dalloc(&e->region_start, padded);
-    if (rc == RL_OK) rc = dalloc(&e->row_tmp, padded / 4096 + 1);
-    if (rc == RL_OK) rc = dalloc(&e->row_base, padded / 4096 + 1);
-    if (rc != RL_OK) return rc;
-    e->region_cap = padded;
+// rstart / rend per bin for two-pass partitions (k_bin_bounds).
+static int ensure_regions(rl_engine* e, size_t bins) {
+    if (bins <= e->region_cap) return RL_OK;
+    dfree(e->region_count); dfree(e->region_start);
+    int rc = dalloc(&e->region_count, bins);
+    if (rc == RL_OK) rc = dalloc(&e->region_start, bins);
+    if (rc != RL_OK) { e->region_cap = 0; return rc; }
+    e->region_cap = bins;
     return RL_OK;
 }
 
-static inline void mark(rl_engine* e, int i) {
-    if (e->timing) (void)hipEventRecord(e->ev[e->ring_next][i], e->stream);
+static int ensure_hot_summ(rl_engine* e, size_t n) {
+    const size_t need = n / kHotChunk + kHotMax + 1;
+    if (need <= e->hot_summ_cap) return RL_OK;
+    dfree(e->hot_summ);
+    if (dalloc(&e->hot_summ, need * 4) != RL_OK) { e->hot_summ_cap = 0; return RL_E_NOMEM; }
+    e->hot_summ_cap = need;
+    return RL_OK;
 }
+
+static int ensure_hot_mark(rl_engine* e, size_t bins) {
+    if (bins <= e->hot_mark_cap) return RL_OK;
+    dfree(e->hot_mark);
+    if (dalloc(&e->hot_mark, bins) != RL_OK) { e->hot_mark_cap = 0; return RL_E_NOMEM; }
+    HIP_OK(hipMemset(e->hot_mark, 0, bins * sizeof(uint32_t)));
+    e->hot_mark_cap = bins;
+    e->epoch = 0;
+    return RL_OK;
+}
+
+static inline void mark_on(rl_engine* e, int i, hipStream_t st) {
+    if (e->timing) (void)hipEventRecord(e->ev[e->ring_next][i], st);
+}
+static inline void mark(rl_engine* e, int i) { mark_on(e, i, e->stream); }
 
 // The pipeline on device buffers, enqueued on e->stream. Returns an immediate status
 // (argument/launch errors); the data-dependent status is read back by rl_last_status.
@@ -372,11 +421,19 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     const int d1 = bitsP - d0;
     int rc = ensure_scratch(e, n, wide, 1u << std::max(d0, d1), nt);
     if (rc != RL_OK) return rc;
-    const uint32_t cols = 4096;
-    const size_t padded = ((size_t)n_bins + cols - 1) / cols * cols;
     if (passes == 2) {
-        rc = ensure_regions(e, padded);
+        rc = ensure_regions(e, n_bins);
         if (rc != RL_OK) return rc;
+    }
+    const bool hot = e->hot_threshold > 0 && bsh == 0;
+    if (hot) {
+        rc = ensure_hot_mark(e, n_bins);
+        if (rc == RL_OK) rc = ensure_hot_summ(e, n);
+        if (rc != RL_OK) return rc;
+        if (++e->epoch == 0) {                       // marks hold epochs: restart after wrap
+            HIP_OK(hipMemsetAsync(e->hot_mark, 0, e->hot_mark_cap * sizeof(uint32_t), s));
+            e->epoch = 1;
+        }
     }
     e->last_wide = wide;
 
@@ -391,10 +448,6 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     // ---- pass 0 (low digit) from the caller's arrays
     pa.digit_shift = 0; pa.digit_bits = d0;
     pa.region_count = nullptr;
-    if (passes == 2) {
-        HIP_OK(hipMemsetAsync(e->region_count, 0, padded * sizeof(uint32_t), s));
-        pa.region_count = e->region_count;
-    }
     pa.rec_out = e->rec0; pa.pos_out = e->pos0;
     HIP_OK(launch_upsweep(pa, true, wide, s));
     mark(e, 1);
@@ -406,10 +459,10 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     const void* rec_final = e->rec0;
     const uint32_t* rstart = e->bin_base;
     const uint32_t* rcount = e->bin_total;
+    const uint32_t* rend = nullptr;
     if (passes == 2) {
         // ---- pass 1 (high digit) over the records; stable, so the final order is
-        // region-major and arrival-ordered inside each region.
-        pa.region_count = nullptr;
+        // bin-major and arrival-ordered inside each bin.
         pa.digit_shift = d0; pa.digit_bits = d1;
         pa.rec_in = e->rec0; pa.rec_out = e->rec1; pa.pos_out = e->pos1;
         HIP_OK(launch_upsweep(pa, false, wide, s));
@@ -425,20 +478,56 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     mark(e, 6);
     if (passes == 2) {
-        const uint32_t rows = (uint32_t)(padded / cols);
-        HIP_OK(launch_scan_rows(e->region_count, e->region_start, rows, cols, e->row_tmp, s));
-        HIP_OK(launch_scan_small(e->row_tmp, e->row_base, rows, s));
-        HIP_OK(launch_add_rows(e->row_base, e->region_start, rows, cols, s));
+        // bin boundaries from the final order (no per-request atomics: a hot bin would
+        // serialise them)
+        HIP_OK(hipMemsetAsync(e->region_start, 0, (size_t)n_bins * sizeof(uint32_t), s));
+        HIP_OK(hipMemsetAsync(e->region_count, 0, (size_t)n_bins * sizeof(uint32_t), s));
+        BoundsArgs ba{};
+        ba.rec = rec_final; ba.n = (uint32_t)n; ba.n_lim = (uint32_t)e->lims.size();
+        ba.lims = e->d_lims; ba.shard_bits = e->shard_bits; ba.bin_shift = bsh;
+        ba.rstart = e->region_start; ba.rend = e->region_count;
+        HIP_OK(launch_bin_bounds(ba, wide, s));
         rstart = e->region_start;
-        rcount = e->region_count;
+        rcount = nullptr;
+        rend = e->region_count;
     }
-    mark(e, 7);
     RegionArgs ra{};
-    ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.region_lim = e->d_region_lim;
+    ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.rend = rend;
+    ra.region_lim = e->d_region_lim;
     ra.lims = e->d_lims; ra.res = e->res; ra.tok = tokens_after ? e->tok : nullptr;
     ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
+    if (e->debug_regions) {
+        if (e->dbg_cap < (size_t)n_bins * 4) {
+            dfree(e->dbg);
+            if (dalloc(&e->dbg, (size_t)n_bins * 4) != RL_OK) { e->dbg_cap = 0; return RL_E_NOMEM; }
+            e->dbg_cap = (size_t)n_bins * 4;
+        }
+        HIP_OK(hipMemsetAsync(e->dbg, 0, e->dbg_cap * sizeof(uint64_t), s));
+        ra.dbg = e->dbg;
+    }
+    if (hot) {
+        uint32_t* hot_count = e->hot_list + kHotMax;
+        HIP_OK(hipMemsetAsync(hot_count, 0, 34 * sizeof(uint32_t), s));
+        HIP_OK(launch_hot_select(rstart, rcount, rend, n_bins, e->hot_threshold, e->hot_list,
+                                 hot_count, e->hot_mark, e->epoch, s));
+        ra.hot_list = e->hot_list; ra.hot_count = hot_count; ra.hot_mark = e->hot_mark;
+        ra.epoch = e->epoch;
+        ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ; ra.hot_total = e->hot_list + kHotMax + 36;
+        HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
+        HIP_OK(hipEventRecord(e->ev_fork, s));
+        HIP_OK(hipStreamWaitEvent(e->stream_hot, e->ev_fork, 0));
+        mark_on(e, 10, e->stream_hot);
+        HIP_OK(launch_hot_chain(ra, wide, res_bytes, e->stream_hot));
+        mark_on(e, 11, e->stream_hot);
+        HIP_OK(hipEventRecord(e->ev_join, e->stream_hot));
+    } else {
+        mark_on(e, 10, s);
+        mark_on(e, 11, s);
+    }
+    mark(e, 7);
     HIP_OK(launch_region(ra, wide, res_bytes, s));
+    if (hot) HIP_OK(hipStreamWaitEvent(s, e->ev_join, 0));
     mark(e, 8);
     UnpermArgs ua{};
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
@@ -626,6 +715,12 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "upsweep_per_cu") == 0) { e->up_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "scatter_per_cu") == 0) { e->sc_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "unpermute_per_cu") == 0) { e->un_per_cu = (uint32_t)value; return RL_OK; }
+    if (std::strcmp(key, "debug_regions") == 0) { e->debug_regions = value != 0; return RL_OK; }
+    if (std::strcmp(key, "hot_threshold") == 0) {      // records per region; 0 = no hot path
+        if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
+        e->hot_threshold = (uint32_t)value;
+        return RL_OK;
+    }
     if (std::strcmp(key, "bin_shift") == 0) {
         if (value != 0 && value != kBinShift) return RL_E_INVALID_ARG;
         e->bin_shift = (int)value;
@@ -728,4 +823,17 @@ extern "C" int rl_synth_trace_device(rl_engine* e, const rl_trace_spec* sp, size
     hipStream_t st = stream ? (hipStream_t)stream : e->stream;
     HIP_OK(launch_synth(a, st));
     return RL_OK;
+}
+
+extern "C" int rl_debug_fetch(rl_engine* e, const char* what, void* out, size_t bytes) {
+    if (!e || !what || (!out && bytes)) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (std::strcmp(what, "region_times") == 0) {
+        if (!e->dbg) return RL_E_INVALID_ARG;
+        HIP_OK(hipStreamSynchronize(e->stream));
+        const size_t nb = std::min(bytes, e->dbg_cap * sizeof(uint64_t));
+        HIP_OK(hipMemcpy(out, e->dbg, nb, hipMemcpyDeviceToHost));
+        return (int)(nb / (4 * sizeof(uint64_t)));
+    }
+    return RL_E_INVALID_ARG;
 }

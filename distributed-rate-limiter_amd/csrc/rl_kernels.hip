@@ -390,7 +390,7 @@ template <class Codec, int ALGO, class LdsT>
 __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimiter& L,
                                      uint32_t lane, const typename Codec::Rec& cur, bool valid,
                                      uint32_t j, int64_t base, uint32_t pad, uint32_t& n_allowed,
-                                     uint32_t& n_invalid, uint32_t& n_caperr) {
+                                     uint32_t& n_invalid, uint32_t& n_caperr, uint32_t& n_rounds) {
     constexpr uint32_t NS = kRegionSlots;
     constexpr bool tb = ALGO == kAlgoTB;        // per-algorithm code: nothing of the other
     Applied r;
@@ -450,6 +450,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                                      : wave_match((uint32_t)slot, kRegionBits, slot >= 0);
     bool pending = slot >= 0;
     while (__any(pending)) {
+        ++n_rounds;
         Outcome o{};
         if (pending) {
             if (a.ablate & kAblNoStep) {
@@ -489,9 +490,10 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
     const uint32_t rb = RPB == 1 ? 0u : (g / 8) % 8;
     const uint32_t n_bins = a.n_regions / RPB;
     if (bin >= n_bins) return;
-    const uint32_t cnt = a.rcount[bin];
-    if (cnt == 0) return;
+    if (a.hot_mark && a.hot_mark[bin] == a.epoch) return;     // owned by k_regions_hot
     const uint32_t start = a.rstart[bin];
+    const uint32_t cnt = a.rend ? a.rend[bin] - start : a.rcount[bin];
+    if (cnt == 0) return;
     const uint32_t end = start + cnt;
     const uint32_t lane = threadIdx.x;
     const uint32_t region = bin * RPB + rb;
@@ -541,7 +543,8 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
     }
     wave_fence();
 
-    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0;
+    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0;
+    const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t head = 0, count = 0;                    // ring state (wave-uniform)
     // the whole stream is instantiated once per algorithm (uniform per region), so the
     // compiler hoists nothing of the other algorithm into the hot loop
@@ -552,7 +555,7 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
             if constexpr (RPB == 1) {
                 // the bin is the region: every record is ours, applied straight from registers
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, idx < end, idx, base, pad,
-                                                     n_allowed, n_invalid, n_caperr);
+                                                     n_allowed, n_invalid, n_caperr, n_rounds);
                 res[ap.j] = (Res)ap.out;
                 if (TOK) a.tok[ap.j] = ap.tok;
             } else {
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
                 if (count >= 64) {
                     const uint32_t ri = (head + lane) % kRing;
                     ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
-                                           n_allowed, n_invalid, n_caperr);
+                                           n_allowed, n_invalid, n_caperr, n_rounds);
                     head = (head + 64) % kRing;
                     count -= 64;
                 }
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
                 const bool v = lane < count;
                 const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
-                                                     pad, n_allowed, n_invalid, n_caperr);
+                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds);
                 res[ap.j] = (Res)ap.out;
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
@@ -630,6 +633,518 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
         if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
         atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
         atomicAdd(&a.ctl->regions, 1ULL);
+        if (a.dbg) {
+            uint64_t* d = a.dbg + (size_t)bin * 4;
+            d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = cnt; d[3] = n_rounds;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 4b. hot regions
+// A region far above the average share (a hot Zipf key: at s = 1.1 over 100M keys the
+// top key draws 11 % of all requests) would serialise one wave, and one CU's memory
+// bandwidth, for the whole batch. Its dominant key (the HOT key) gets a fast path:
+//  * a deny never changes state (SlidingWindowRateLimiter.java:104-111,
+//    TokenBucketRateLimiter.java:61-67);
+//  * for a fixed state the SW estimate (:158-180) is non-increasing in `now` for `now`
+//    at or after the newest bucket, and the TB balance (Lua :46-58) is non-decreasing.
+// So one threshold pair [T0, T1) per state holds exactly the times at which a request is
+// denied with remaining 0 (SW: est >= max; TB: 0 <= balance < 1), whatever its permits.
+// Requests outside it (the next allow, denials with remaining > 0, peeks, resets) run
+// the exact step one at a time in arrival order; after a state change T1 is found again
+// by an exact search that evaluates the very same arithmetic (tb_refill, sw_estimate) at
+// 64 times per wave instruction. Three phases:
+//  A  k_hot_summ  (all CUs)  per 64 records: time range of the hot key's plain acquires,
+//                             count of records that need the exact path;
+//  B  k_hot_chain (one wave per hot region, beside k_regions) walks the summaries with
+//                             [T0, T1), decides whole chunks unread, processes the rest
+//                             record by record (other keys through wave_apply);
+//  C  k_hot_fill  (all CUs)  writes the results of the decided chunks.
+template <int ALGO>
+__device__ inline bool hot_pred(const DevLimiter& L, int64_t t, uint64_t a, uint64_t b, uint64_t c) {
+    if constexpr (ALGO == kAlgoTB) {
+        return tb_refill(L, t, a, b, c) >= 1.0;
+    } else {
+        const SW2 s = sw_unpack(a, b, c);
+        return sw_estimate(s, sw_geo(t, L.window_ms), t, L.window_ms) < L.max_permits;
+    }
+}
+
+// Start of the range on which hot_pred is monotone and the fast result is valid.
+template <int ALGO>
+__device__ inline int64_t hot_t0(int64_t lo, int64_t hi, uint64_t a, uint64_t b, uint64_t c) {
+    if constexpr (ALGO == kAlgoTB) {
+        if (!(c & 1u)) return lo;                               // absent: full at every t
+        if (!(__longlong_as_double((long long)a) >= 0.0)) return hi + 1;
+        return (int64_t)b > lo ? (int64_t)b : lo;               // t >= last: balance >= 0
+    } else {
+        const SW2 s = sw_unpack(a, b, c);
+        if (s.b1_cnt == 0 && s.b0_cnt == 0) return lo;
+        return s.b1_start > lo ? s.b1_start : lo;
+    }
+}
+
+// First t in [s, hi] with pred(t) for a predicate monotone (false..true) on [s, hi];
+// hi + 1 if none. One wave: an exponential bracket (64 probes in one instruction), then
+// 64-ary narrowing. Arguments are wave-uniform.
+template <class P>
+__device__ inline int64_t wave_first_true(int64_t s, int64_t hi, uint32_t lane, P pred) {
+    if (s > hi) return hi + 1;
+    int64_t t = lane == 0 ? s : (lane < 63 ? s + ((int64_t)1 << (lane - 1)) : hi);
+    if (t > hi) t = hi;
+    const uint64_t m = __ballot(pred(t));
+    if (m == 0) return hi + 1;
+    const uint32_t k = (uint32_t)__builtin_ctzll(m);
+    if (k == 0) return s;
+    int64_t lo = __shfl(t, (int)k - 1, 64) + 1;                 // pred(t_{k-1}) false
+    int64_t h = __shfl(t, (int)k, 64);                          // pred(t_k) true
+    while (h > lo) {
+        const int64_t step = (h - lo + 64) / 64;
+        int64_t u = lo + ((int64_t)lane + 1) * step - 1;
+        if (u > h) u = h;
+        const uint64_t mm = __ballot(pred(u));
+        if (mm == 0) return h;                                  // (monotone: not reached)
+        const uint32_t kk = (uint32_t)__builtin_ctzll(mm);
+        const int64_t uk = __shfl(u, (int)kk, 64);
+        const int64_t ukm = __shfl(u, kk ? (int)kk - 1 : 0, 64);
+        lo = kk ? ukm + 1 : lo;
+        h = uk;
+    }
+    return lo;
+}
+
+template <int ALGO>
+__device__ inline void hot_thresholds(const DevLimiter& L, uint64_t a, uint64_t b, uint64_t c,
+                                      int64_t from, int64_t lo, int64_t hi, uint32_t lane,
+                                      int64_t* T0, int64_t* T1) {
+    const int64_t t0 = hot_t0<ALGO>(lo, hi, a, b, c);
+    const int64_t s = from > t0 ? from : t0;
+    int64_t t1 = wave_first_true(s, hi, lane, [&](int64_t t) { return hot_pred<ALGO>(L, t, a, b, c); });
+    if (t1 == s) t1 = t0;        // pred(s) already true: [t0, s) undecided -> empty range
+    *T0 = t0;
+    *T1 = t1;
+}
+
+// Lane order = arrival order; chunk g of the listed regions -> (region i, chunk c).
+__device__ inline uint32_t hot_region_of(const uint32_t* s_base, uint32_t hc, uint32_t g) {
+    uint32_t lo = 0, hi = hc;                        // last i with s_base[i] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (s_base[mid] <= g) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Phase 0 (one wave per listed region): bounds, chunks and the dominant key of a sample
+// of the region's first 64 records (a hot region is dominated by its hot key).
+template <class Codec>
+__global__ __launch_bounds__(64) void k_hot_prep(RegionArgs a) {
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    const uint32_t i = blockIdx.x, lane = threadIdx.x;
+    if (i >= hc) return;
+    const uint32_t bin = a.hot_list[i];
+    const uint32_t start = a.rstart[bin];
+    const uint32_t end = start + (a.rend ? a.rend[bin] - start : a.rcount[bin]);
+    const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
+    const int64_t base = a.ctl->base_ms;
+    const uint32_t n0 = min(end - start, 64u);
+    const bool act = lane < n0;
+    uint64_t h = 0;
+    bool ok = false;
+    if (act) {
+        const Req q = Codec::dec(recs[start + lane], base);
+        h = q.h;
+        ok = !q.invalid;
+    }
+    uint32_t cnt = 0;
+    for (uint32_t k = 0; k < n0; ++k) cnt += (__shfl(h, (int)k, 64) == h) ? 1u : 0u;
+    uint32_t key = (act && ok) ? (cnt << 6) | (63u - lane) : 0u;
+    for (int o = 32; o > 0; o >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, o, 64));
+    const uint64_t tag = __shfl(h, (int)(63u - (key & 63u)), 64);
+    if (lane == 0) {
+        HotInfo f;
+        f.tag = tag; f.bin = bin; f.start = start; f.end = end;
+        f.n_chunks = (end - start + kHotChunk - 1) / kHotChunk;
+        f.chunk_base = 0;
+        f.ok = (key >> 6) >= 2u ? 1u : 0u;
+        a.hot_info[i] = f;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_hot_scan(RegionArgs a) {
+    __shared__ uint32_t tmp[16];
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    const uint32_t t = threadIdx.x;
+    const uint32_t v = t < hc ? a.hot_info[t].n_chunks : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan<1024>(v, tmp, &tot);
+    if (t < hc) a.hot_info[t].chunk_base = ex;
+    if (t == 0) *a.hot_total = tot;
+}
+
+// Phase A (one wave per 64-record chunk, all CUs): what the chain needs to decide a chunk
+// without reading it: the time range of the hot key's plain acquires, and how many
+// records need the exact path (other keys, invalid, peek / reset of the hot key).
+// Summary words: [0] min now, [1] max now, [2] n_special | n_hot << 8 | n_early << 16,
+// [3] verdict (k_hot_chain: 1 = decided by the thresholds, words 0-2 then hold the state).
+template <class Codec>
+__global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
+    __shared__ uint32_t s_base[kHotMax + 1];
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    const uint32_t total = *a.hot_total;
+    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].chunk_base;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
+    const int64_t base = a.ctl->base_ms;
+    for (uint32_t g = blockIdx.x * 4 + wid; g < total; g += gridDim.x * 4) {
+        const uint32_t i = hot_region_of(s_base, hc, g);
+        const HotInfo f = a.hot_info[i];
+        const DevLimiter& L = a.lims[a.region_lim[f.bin]];
+        const uint32_t j = f.start + (g - s_base[i]) * kHotChunk + lane;
+        const bool valid = j < f.end;
+        Req q{};
+        if (valid) q = Codec::dec(recs[j], base);
+        const bool hot = valid && f.ok && !q.invalid && q.h == f.tag;
+        const bool acq = q.op == (uint32_t)kOpAcquire;
+        const bool early = hot && acq && L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
+        const bool plain = hot && acq && !early;
+        const bool special = valid && !(hot && acq);
+        uint64_t mn = plain ? ord_key(q.now_ms) : ~0ULL, mx = plain ? ord_key(q.now_ms) : 0ULL;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t x = __shfl_xor(mn, o, 64), y = __shfl_xor(mx, o, 64);
+            mn = x < mn ? x : mn;
+            mx = y > mx ? y : mx;
+        }
+        const uint32_t ns = (uint32_t)__popcll(__ballot(special));
+        const uint32_t nh = (uint32_t)__popcll(__ballot(hot));
+        const uint32_t ne = (uint32_t)__popcll(__ballot(early));
+        if (lane == 0) {
+            uint64_t* d = a.hot_summ + (size_t)g * 4;
+            d[0] = mn == ~0ULL ? (uint64_t)INT64_MAX : (mn ^ 0x8000000000000000ULL);
+            d[1] = mx == 0ULL ? (uint64_t)INT64_MIN : (mx ^ 0x8000000000000000ULL);
+            d[2] = ns | (nh << 8) | (ne << 16);
+            d[3] = 0;
+        }
+    }
+}
+
+// Phase B (one wave per listed region, beside k_regions): walks the region's chunk
+// summaries in arrival order with the hot key's threshold pair; a chunk whose hot-key
+// times all lie in [T0, T1) and that holds nothing else is decided without being read
+// (its verdict + the key's state go back into the summary for k_hot_fill). Any other
+// chunk is processed here record by record: the hot key through the fast check and the
+// wavefront-per-key sequential run, the other keys through wave_apply.
+template <class Codec, class Res, bool TOK>
+__global__ __launch_bounds__(64) void k_hot_chain(RegionArgs a) {
+    using Rec = typename Codec::Rec;
+    constexpr uint32_t NS = kRegionSlots;
+    __shared__ RegionTable S;
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    const uint32_t i = blockIdx.x, lane = threadIdx.x;
+    if (i >= hc) return;
+    const HotInfo f = a.hot_info[i];
+    const uint32_t region = f.bin;                    // bin_shift 0: bin == region
+    const DevLimiter L = a.lims[a.region_lim[region]];
+    const int64_t base = a.ctl->base_ms;
+    const int64_t lo = (int64_t)(a.ctl->min_now_key ^ 0x8000000000000000ULL);
+    const int64_t hi = (int64_t)(a.ctl->max_now_key ^ 0x8000000000000000ULL);
+    const Rec* recs = (const Rec*)a.rec;
+    Res* res = (Res*)a.res;
+    const uint32_t pad = a.n_total + lane;
+    if (a.ctl->span_overflow != 0) {                  // whole batch rejected (see k_regions)
+        for (uint32_t j = f.start + lane; j < f.end; j += 64) {
+            res[j] = (Res)pack_result(false, kRemInvalid);
+            if (TOK) a.tok[j] = __builtin_nan("");
+        }
+        return;
+    }
+    const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    // ---- load + rebuild the region (as k_regions), find or insert the hot key's slot
+    Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
+    Slot img[NS / 64];
+#pragma unroll
+    for (uint32_t k = 0; k < NS / 64; ++k) {
+        S.occ[lane + 64 * k] = 0;
+        img[k] = tab[lane + 64 * k];
+    }
+    wave_fence();
+#pragma unroll
+    for (uint32_t k = 0; k < NS / 64; ++k) {
+        const Slot v = img[k];
+        if (slot_live(L, v, lo)) {
+            uint32_t p = slot_home(v.tag);
+            while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+            S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
+        }
+    }
+    wave_fence();
+    int32_t hslot = -1;
+    if (f.ok) {
+        const uint32_t p0 = slot_home(f.tag);
+        for (uint32_t k = 0; k < NS; ++k) {                 // linear probing, as the rebuild
+            const uint32_t p = (p0 + k) & (NS - 1);
+            const uint32_t o = S.occ[p];
+            if (!(o & 1u) || S.tag[p] == f.tag) { hslot = (int32_t)p; break; }
+        }
+        if (hslot >= 0 && !(S.occ[hslot] & 1u)) {
+            wave_fence();
+            if (lane == 0) {
+                S.occ[hslot] = 1u; S.tag[hslot] = f.tag; S.sa[hslot] = 0; S.sb[hslot] = 0; S.sc[hslot] = 0;
+            }
+            wave_fence();
+        }
+    }
+    const bool hot_ok = hslot >= 0;
+    const uint32_t hs = hot_ok ? (uint32_t)hslot : 0u;
+    const uint64_t tag = f.tag;
+
+    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0;
+    bool any_hot = false;
+    auto body = [&](auto algo) {
+        constexpr int A = decltype(algo)::value;
+        int64_t T0 = lo, T1 = lo;                         // empty range until computed
+        if (hot_ok) hot_thresholds<A>(L, S.sa[hs], S.sb[hs], S.sc[hs], lo, lo, hi, lane, &T0, &T1);
+        // one chunk, record by record (lane = arrival order inside the chunk)
+        auto detail = [&](uint32_t c) {
+            ++n_detail;
+            const uint32_t j = f.start + c * kHotChunk + lane;
+            const bool valid = j < f.end;
+            const Rec r = recs[valid ? j : f.start];
+            const Req q = Codec::dec(r, base);
+            const bool hot = hot_ok && valid && !q.invalid && q.h == tag;
+            uint64_t out = 0;
+            double tk = __builtin_nan("");
+            bool pend = hot;
+            if (A == kAlgoTB && hot && q.op == (uint32_t)kOpAcquire && (int64_t)q.permits > L.max_permits) {
+                out = pack_result(false, kRemUnknown);    // :110-116, no state access
+                pend = false;
+            }
+            for (;;) {
+                const bool fast = q.op == (uint32_t)kOpAcquire && q.now_ms >= T0 && q.now_ms < T1;
+                const uint64_t m = __ballot(pend && !fast);
+                const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+                if (pend && lane < first) {               // inside [T0, T1): denied, remaining 0
+                    out = pack_result(false, 0);
+                    if (TOK && A == kAlgoTB) tk = tb_refill(L, q.now_ms, S.sa[hs], S.sb[hs], S.sc[hs]);
+                    pend = false;
+                }
+                if (first == 64u) break;
+                // sequential run from `first`, state in registers, until a (deny, 0)
+                const uint64_t pm = __ballot(pend);
+                uint64_t sa = S.sa[hs], sb = S.sb[hs], sc = S.sc[hs];
+                uint32_t flag = 0;
+                int64_t from = 0;
+                for (uint32_t jj = first; jj < 64; ++jj) {
+                    if (!((pm >> jj) & 1u)) continue;
+                    const int64_t now = __shfl(q.now_ms, (int)jj, 64);
+                    const int32_t pj = __shfl(q.permits, (int)jj, 64);
+                    const uint32_t op = (uint32_t)__shfl((int)q.op, (int)jj, 64);
+                    Outcome o;
+                    if constexpr (A == kAlgoTB) o = tb_step(L, op, pj, now, sa, sb, sc);
+                    else o = sw_step(L, op, pj, now, sa, sb, sc);
+                    if (o.mutate) { sa = o.a; sb = o.b; sc = o.c; flag |= 1u; }
+                    if (lane == jj) { out = pack_result(o.allowed, o.remaining); tk = o.tokens; pend = false; }
+                    if (lane == 0 && o.allowed) ++n_allowed;
+                    if (!o.mutate && !o.allowed && o.remaining == 0 && op == (uint32_t)kOpAcquire) {
+                        flag |= 2u;
+                        from = now;
+                        break;
+                    }
+                }
+                wave_fence();
+                if (lane == 0) { S.sa[hs] = sa; S.sb[hs] = sb; S.sc[hs] = sc; }
+                wave_fence();
+                if (flag & 2u) hot_thresholds<A>(L, sa, sb, sc, from, lo, hi, lane, &T0, &T1);
+                else if (flag & 1u) T1 = T0;              // changed state: no fast range yet
+            }
+            const bool nonhot = valid && !hot;
+            if (__any(nonhot)) {                          // every other key of the region
+                const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, nonhot, j, base, pad,
+                                                        n_allowed, n_invalid, n_caperr, n_rounds);
+                if (nonhot) { out = ap.out; tk = ap.tok; }
+            }
+            if (valid) {
+                res[j] = (Res)out;
+                if (TOK) a.tok[j] = tk;
+            }
+        };
+        for (uint32_t c0 = 0; c0 < f.n_chunks; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            const bool has = c < f.n_chunks;
+            uint64_t* sm = a.hot_summ + (size_t)(f.chunk_base + (has ? c : 0)) * 4;
+            int64_t mn = INT64_MAX, mx = INT64_MIN;
+            uint32_t ns = 0, ne = 0;
+            if (has) {
+                mn = (int64_t)sm[0];
+                mx = (int64_t)sm[1];
+                const uint32_t w = (uint32_t)sm[2];
+                ns = w & 0xFFu;
+                ne = (w >> 16) & 0xFFu;
+                any_hot |= ((w >> 8) & 0xFFu) != 0;
+            }
+            uint64_t todo = __ballot(has);
+            while (todo) {
+                const bool skip = ns == 0 && mn >= T0 && mx < T1;
+                const uint64_t nsk = todo & ~__ballot(skip);
+                const uint32_t fst = nsk ? (uint32_t)__builtin_ctzll(nsk) : 64u;
+                if (((todo >> lane) & 1u) && lane < fst) {      // decided: state is constant here
+                    sm[0] = S.sa[hs]; sm[1] = S.sb[hs]; sm[2] = S.sc[hs]; sm[3] = ne ? 3u : 1u;
+                }
+                if (fst == 64u) break;
+                todo &= fst == 63u ? 0ULL : ~((2ULL << fst) - 1);
+                detail(c0 + fst);
+            }
+        }
+    };
+    if (L.algo == kAlgoTB) body(std::integral_constant<int, kAlgoTB>{});
+    else body(std::integral_constant<int, kAlgoSW>{});
+    // ---- write the region back, statistics
+    const bool touched_hot = __any(any_hot);
+    wave_fence();
+    if (lane == 0 && hot_ok && touched_hot) S.occ[hs] |= 2u;
+    wave_fence();
+    uint32_t touched = 0;
+    for (uint32_t sl = lane; sl < NS; sl += 64) {
+        const uint32_t o = S.occ[sl];
+        Slot v;
+        if (o & 1u) { v.tag = S.tag[sl]; v.a = S.sa[sl]; v.b = S.sb[sl]; v.c = S.sc[sl]; }
+        else { v.tag = 0; v.a = 0; v.b = 0; v.c = 0; }
+        tab[sl] = v;
+        touched += (o >> 1) & 1u;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        n_allowed += __shfl_xor(n_allowed, off, 64);
+        n_invalid += __shfl_xor(n_invalid, off, 64);
+        n_caperr += __shfl_xor(n_caperr, off, 64);
+        touched += __shfl_xor(touched, off, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
+        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
+        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
+        atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
+        atomicAdd(&a.ctl->regions, 1ULL);
+        if (a.dbg) {
+            uint64_t* d = a.dbg + (size_t)region * 4;
+            d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = f.end - f.start;
+            d[3] = (uint64_t)n_detail | (1ULL << 63);     // top bit: a hot region; low: detailed chunks
+        }
+    }
+}
+
+// Phase C (one wave per chunk, all CUs): results of the chunks the chain decided.
+template <class Codec, class Res, bool TOK>
+__global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
+    __shared__ uint32_t s_base[kHotMax + 1];
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    const uint32_t total = *a.hot_total;
+    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].chunk_base;
+    __syncthreads();
+    if (a.ctl->span_overflow != 0) return;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
+    const int64_t base = a.ctl->base_ms;
+    Res* res = (Res*)a.res;
+    for (uint32_t g = blockIdx.x * 4 + wid; g < total; g += gridDim.x * 4) {
+        const uint64_t* sm = a.hot_summ + (size_t)g * 4;
+        if (!(sm[3] & 1u)) continue;
+        const uint32_t i = hot_region_of(s_base, hc, g);
+        const HotInfo f = a.hot_info[i];
+        const uint32_t j = f.start + (g - s_base[i]) * kHotChunk + lane;
+        if (j >= f.end) continue;
+        // every record here is the hot key's acquire (n_special == 0); TB permits > max
+        // (verdict bit 1) are the only ones not (deny, 0)
+        const DevLimiter& L = a.lims[a.region_lim[f.bin]];
+        if (!TOK && !(sm[3] & 2u)) {
+            res[j] = (Res)pack_result(false, 0);
+            continue;
+        }
+        const Req q = Codec::dec(recs[j], base);
+        const bool early = L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
+        res[j] = (Res)pack_result(false, early ? kRemUnknown : 0);
+        if (TOK) a.tok[j] = (L.algo == kAlgoTB && !early) ? tb_refill(L, q.now_ms, sm[0], sm[1], sm[2])
+                                                         : __builtin_nan("");
+    }
+}
+
+// Hot-region selection, largest first: k_hot_hist counts the bins at or above the
+// threshold per power-of-two size class; k_hot_select then raises the threshold to the
+// smallest class boundary that admits at most kHotMax bins and lists those bins.
+// hot_meta: [0] listed count, [1 .. 33] size-class histogram.
+__device__ inline uint32_t bin_records(const uint32_t* rstart, const uint32_t* rcount,
+                                       const uint32_t* rend, uint32_t b) {
+    return rend ? rend[b] - rstart[b] : rcount[b];
+}
+
+__global__ __launch_bounds__(256) void k_hot_hist(const uint32_t* rstart, const uint32_t* rcount,
+                                                  const uint32_t* rend, uint32_t n_bins,
+                                                  uint32_t threshold, uint32_t* hot_meta) {
+    __shared__ uint32_t h[33];
+    if (threadIdx.x < 33) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b < n_bins) {
+        const uint32_t cnt = bin_records(rstart, rcount, rend, b);
+        if (cnt >= threshold && cnt > 0) atomicAdd(&h[31 - __builtin_clz(cnt)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 33 && h[threadIdx.x]) atomicAdd(&hot_meta[1 + threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, const uint32_t* rcount,
+                                                    const uint32_t* rend, uint32_t n_bins,
+                                                    uint32_t threshold, uint32_t* hot_list,
+                                                    uint32_t* hot_meta, uint32_t* hot_mark,
+                                                    uint32_t epoch) {
+    __shared__ uint32_t s_thr;
+    if (threadIdx.x == 0) {
+        uint32_t above = 0, thr = 0xFFFFFFFFu;
+        for (int c = 32; c >= 0; --c) {               // classes from the largest down
+            above += hot_meta[1 + c];
+            if (above > kHotMax) break;
+            thr = c == 0 ? 1u : (1u << c);
+        }
+        s_thr = thr > threshold ? thr : threshold;
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= n_bins) return;
+    const uint32_t cnt = bin_records(rstart, rcount, rend, b);
+    if (cnt == 0 || cnt < s_thr) return;
+    const uint32_t k = atomicAdd(&hot_meta[0], 1u);
+    if (k < kHotMax) {                                // (always, by the choice of s_thr)
+        hot_list[k] = b;
+        hot_mark[b] = epoch;
+    }
+}
+
+// Bin boundaries of the final record order (two-pass partitions): rstart[b] / rend[b]
+// for every bin that holds records (both arrays zeroed before, so empty bins read 0).
+template <class Codec>
+__global__ __launch_bounds__(256) void k_bin_bounds(BoundsArgs a) {
+    __shared__ uint32_t s_base[256];
+    __shared__ uint8_t s_bits[256];
+    for (uint32_t l = threadIdx.x; l < a.n_lim; l += 256) {
+        s_base[l] = a.lims[l].region_base;
+        s_bits[l] = (uint8_t)a.lims[l].region_bits;
+    }
+    __syncthreads();
+    const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
+    auto bin = [&](uint32_t i) {
+        const typename Codec::Rec r = recs[i];
+        const uint32_t lim = Codec::limiter_of(r);
+        return (s_base[lim] + region_local(r.h, a.shard_bits, s_bits[lim])) >> a.bin_shift;
+    };
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t b = i < a.n ? bin(i) : kNone;
+    uint32_t bp = __shfl_up(b, 1, 64), bn = __shfl_down(b, 1, 64);
+    if (lane == 0) bp = (i > 0 && i - 1 < a.n) ? bin(i - 1) : kNone;
+    if (lane == 63) bn = i + 1 < a.n ? bin(i + 1) : kNone;
+    if (i < a.n) {
+        if (b != bp) a.rstart[b] = i;
+        if (b != bn) a.rend[b] = i + 1;
     }
 }
 
@@ -944,6 +1459,55 @@ hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStrea
     else if (res_bytes == 1) region_launch<CodecC, uint8_t>(a, s);
     else if (res_bytes == 2) region_launch<CodecC, uint16_t>(a, s);
     else region_launch<CodecC, uint32_t>(a, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s) {
+    const dim3 gp(persistent_grid(1u << 30, 4));
+    if (wide) hipLaunchKernelGGL(k_hot_prep<CodecW>, dim3(kHotMax), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_hot_prep<CodecC>, dim3(kHotMax), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hot_scan, dim3(1), dim3(1024), 0, s, a);
+    if (wide) hipLaunchKernelGGL(k_hot_summ<CodecW>, gp, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_hot_summ<CodecC>, gp, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+template <class Codec, class Res>
+static void hot_chain_launch(const RegionArgs& a, hipStream_t s) {
+    const dim3 gp(persistent_grid(1u << 30, 4));
+    if (a.tok) {
+        hipLaunchKernelGGL((k_hot_chain<Codec, Res, true>), dim3(kHotMax), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_hot_fill<Codec, Res, true>), gp, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((k_hot_chain<Codec, Res, false>), dim3(kHotMax), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_hot_fill<Codec, Res, false>), gp, dim3(256), 0, s, a);
+    }
+}
+
+hipError_t launch_hot_chain(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
+    if (wide) hot_chain_launch<CodecW, uint64_t>(a, s);
+    else if (res_bytes == 1) hot_chain_launch<CodecC, uint8_t>(a, s);
+    else if (res_bytes == 2) hot_chain_launch<CodecC, uint16_t>(a, s);
+    else hot_chain_launch<CodecC, uint32_t>(a, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
+                             uint32_t n_bins, uint32_t threshold, uint32_t* hot_list,
+                             uint32_t* hot_count, uint32_t* hot_mark, uint32_t epoch,
+                             hipStream_t s) {
+    const dim3 g((n_bins + 255) / 256), b(256);
+    hipLaunchKernelGGL(k_hot_hist, g, b, 0, s, rstart, rcount, rend, n_bins, threshold, hot_count);
+    hipLaunchKernelGGL(k_hot_select, g, b, 0, s, rstart, rcount, rend, n_bins, threshold, hot_list,
+                       hot_count, hot_mark, epoch);
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const dim3 g((a.n + 255) / 256), b(256);
+    if (wide) hipLaunchKernelGGL(k_bin_bounds<CodecW>, g, b, 0, s, a);
+    else hipLaunchKernelGGL(k_bin_bounds<CodecC>, g, b, 0, s, a);
     return hipGetLastError();
 }
 

@@ -62,6 +62,8 @@ struct PartArgs {
     uint32_t ablate;           // rl_tune("ablate"): measurement-only variants (0 = product)
 };
 
+struct HotInfo;
+
 struct RegionArgs {
     const void* rec;           // records in region order
     const uint32_t* rstart;    // [bins] first record of each bin
@@ -76,6 +78,42 @@ struct RegionArgs {
     int32_t shard_bits;
     int32_t bin_shift;
     uint32_t ablate;
+    const uint32_t* rend;      // nullable: bin b holds records [rstart[b], rend[b]) (2 passes)
+    // hot regions (bin_shift 0): k_hot_select lists the largest bins (>= hot_threshold
+    // records, at most kHotMax); the k_hot_* kernels own them (hot_mark[bin] == epoch),
+    // k_regions skips them.
+    const uint32_t* hot_list;  // [kHotMax]
+    const uint32_t* hot_count; // [0]: number listed
+    const uint32_t* hot_mark;  // [bins] nullable
+    uint32_t epoch;
+    HotInfo* hot_info;         // [kHotMax]
+    uint64_t* hot_summ;        // [chunks][4]: k_hot_summ's summary, then k_hot_chain's verdict
+    uint32_t* hot_total;       // total chunks over the listed regions
+    uint64_t* dbg;             // nullable (rl_tune "debug_regions"): per bin {t_start, t_end,
+                               // records, rounds}, t in s_memrealtime ticks (100 MHz)
+};
+
+constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
+constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
+
+struct HotInfo {             // one listed hot region
+    uint64_t tag;            // its dominant key (mix64 of the key hash)
+    uint32_t bin;
+    uint32_t start, end;     // records [start, end) in bin order
+    uint32_t n_chunks;       // ceil((end - start) / kHotChunk)
+    uint32_t chunk_base;     // index of its first chunk summary
+    uint32_t ok;             // dominant key seen at least twice in the sample
+};
+
+struct BoundsArgs {
+    const void* rec;           // records in final (bin) order
+    uint32_t n;
+    uint32_t n_lim;
+    const DevLimiter* lims;
+    int32_t shard_bits;
+    int32_t bin_shift;
+    uint32_t* rstart;          // [bins], zeroed before
+    uint32_t* rend;            // [bins], zeroed before
 };
 
 struct UnpermArgs {
@@ -119,6 +157,13 @@ hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hi
 hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
                            uint32_t cols, hipStream_t s);
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
+hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s);   // prep, scan, summaries
+hipError_t launch_hot_chain(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);  // chain, fill
+hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
+                             uint32_t n_bins, uint32_t threshold, uint32_t* hot_list,
+                             uint32_t* hot_count, uint32_t* hot_mark, uint32_t epoch,
+                             hipStream_t s);
+hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s);
 hipError_t launch_unpermute(const UnpermArgs& a, int res_bytes, hipStream_t s);
 hipError_t launch_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n,
                                hipStream_t s);

@@ -39,7 +39,7 @@ EXPORTS = [
     "rl_execute_batch", "rl_execute_batch_device", "rl_last_status", "rl_available", "rl_reset",
     "rl_batch_stats_get", "rl_stage_times", "rl_sync", "rl_strerror", "rl_abi_version",
     "rl_owner_of", "rl_route_partition", "rl_synth_trace_device", "rl_tune",
-    "rl_route_pack", "rl_route_fold", "rl_route_unpack",
+    "rl_route_pack", "rl_route_fold", "rl_route_unpack", "rl_debug_fetch",
 ]
 
 
@@ -128,6 +128,7 @@ def lib():
     L.rl_route_pack.argtypes = [vp, sz] + [vp] * 10
     L.rl_route_fold.argtypes = [vp, sz] + [vp] * 4
     L.rl_route_unpack.argtypes = [vp, sz] + [vp] * 5
+    L.rl_debug_fetch.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.rl_synth_trace_device.argtypes = [vp, ctypes.POINTER(TraceSpec), sz, vp, vp, vp, vp, vp]
     _lib = L
     return L
@@ -277,6 +278,14 @@ class Engine:
         st = self._L.rl_tune(self._h, key.encode(), int(value))
         if st != RL_OK:
             raise RlError(st, "rl_tune")
+
+    def debug_region_times(self, n_bins):
+        """Per-bin {t_start, t_end, records, rounds} of the last batch (rl_tune debug_regions)."""
+        out = np.zeros((n_bins, 4), np.uint64)
+        k = self._L.rl_debug_fetch(self._h, b"region_times", _p(out), out.nbytes)
+        if k < 0:
+            raise RlError(k, "rl_debug_fetch")
+        return out[:k]
 
     def sync(self):
         st = self._L.rl_sync(self._h)

@@ -1,0 +1,141 @@
+"""GPU parity of the hot-region path (k_hot_summ / k_hot_chain / k_hot_fill): regions
+holding a hot key are decided chunk by chunk through the threshold fast path, the
+wavefront-per-key sequential run and, for their other keys, wave_apply. Everything is
+compared bit-exactly with the CPU oracle, as in test_gpu_parity.py.
+
+`hot_threshold` is lowered in most cases so that the hot path also takes ordinary
+regions (the largest 1024 per batch), which exercises its general path on every trace
+shape the main suite uses."""
+import numpy as np
+import pytest
+
+import rl_amd
+from oracle.coracle import COracle
+from test_gpu_parity import NS, T0, assert_same, trace
+
+pytestmark = pytest.mark.gpu
+
+
+def run(limiters, tr, batches=1, tune=None, **kw):
+    kw.setdefault("max_batch", 1 << 22)
+    kw.setdefault("capacity", 1 << 14)
+    e = rl_amd.Engine(**kw)
+    for l in limiters:
+        e.add_limiter(*l)
+    for k, v in (tune or {}).items():
+        e.tune(k, v)
+    o = COracle(limiters)
+    n = len(tr[0])
+    cuts = np.linspace(0, n, batches + 1).astype(int)
+    got = [[], [], []]
+    for b in range(batches):
+        sl = slice(cuts[b], cuts[b + 1])
+        a, r, t, st = e.execute(*(x[sl] for x in tr))
+        assert st in (rl_amd.RL_OK, rl_amd.RL_E_INVALID_REQUEST), rl_amd.strerror(st)
+        got[0].append(a); got[1].append(r); got[2].append(t)
+    want = o.run(*tr)
+    return tuple(np.concatenate(g) for g in got), want, e
+
+
+def hot_trace(seed, n, n_keys, hot_share, lim_ids, span_ms, permits_max=4, ops=0.0,
+              hot_keys=1, regress=False):
+    """Uniform background traffic plus `hot_keys` keys that draw `hot_share` of it."""
+    rng = np.random.default_rng(seed)
+    ranks = rng.integers(hot_keys, n_keys, n)
+    hot = rng.random(n) < hot_share
+    ranks[hot] = rng.integers(0, hot_keys, hot.sum())
+    keys = rl_amd.mix64(ranks.astype(np.uint64) + np.uint64(seed << 40))
+    lim = np.asarray(lim_ids, np.uint16)[ranks % len(lim_ids)]
+    t = np.sort(rng.integers(0, span_ms * NS, n))
+    if regress:           # TB has no monotone-time precondition: shuffle some times locally
+        j = rng.integers(0, n - 1, n // 50)
+        t[j], t[j + 1] = t[j + 1].copy(), t[j].copy()
+    now = (T0 * NS + t).astype(np.int64)
+    permits = rng.integers(1, permits_max + 1, n).astype(np.int32)
+    op = np.zeros(n, np.uint8)
+    if ops:
+        u = rng.random(n)
+        op[u < ops] = 1
+        op[u < ops / 3] = 2
+    return keys, permits, now, lim, op
+
+
+@pytest.mark.parametrize("algo", ["sw", "tb"])
+def test_hot_key_at_limit(algo):
+    # one key with 40 % of 1.5M requests over 3 minutes: long deny runs between allows
+    lims = [[rl_amd.SW, 1000, 60000, 0.0]] if algo == "sw" else [[rl_amd.TB, 50, 60000, 10.0]]
+    tr = hot_trace(11, 1_500_000, 50_000, 0.4, [0], 180_000, permits_max=1 if algo == "sw" else 4)
+    got, want, e = run(lims, tr, batches=3, capacity=1 << 17)
+    assert_same(got, want, f"hot {algo}")
+
+
+def test_hot_keys_mixed_limiters_ops():
+    # several hot keys over SW and TB limiters, peeks and resets, tokens compared bit-exactly
+    lims = [[rl_amd.SW, 100, 10_000, 0.0], [rl_amd.TB, 20, 5_000, 3.0], [rl_amd.SW, 5, 1000, 0.0],
+            [rl_amd.TB, 500, 60_000, 50.0]]
+    tr = hot_trace(12, 1_200_000, 20_000, 0.6, [0, 1, 2, 3], 120_000, ops=0.01, hot_keys=8)
+    got, want, _ = run(lims, tr, batches=4, tune={"hot_threshold": 4096})
+    assert_same(got, want, "hot mixed")
+
+
+def test_hot_key_under_limit_runs_sequentially():
+    # a hot key that is almost always allowed: every request changes state (wave-per-key run)
+    lims = [[rl_amd.TB, 1_000_000, 60_000, 100_000.0], [rl_amd.SW, 2_000_000, 60_000, 0.0]]
+    tr = hot_trace(13, 400_000, 1_000, 0.5, [0, 1], 30_000, hot_keys=2)
+    got, want, _ = run(lims, tr, batches=2, tune={"hot_threshold": 8192})
+    assert_same(got, want, "hot under limit")
+
+
+def test_hot_tb_time_regression():
+    # TB accepts non-monotone time (negative elapsed, no clamp: Lua :56)
+    lims = [[rl_amd.TB, 30, 20_000, 5.0]]
+    tr = hot_trace(14, 600_000, 5_000, 0.5, [0], 60_000, regress=True)
+    got, want, _ = run(lims, tr, batches=2, tune={"hot_threshold": 4096})
+    assert_same(got, want, "hot regress")
+
+
+@pytest.mark.parametrize("case", ["tb_uniform", "sw_zipf", "mixed_ops"])
+def test_every_region_through_hot_kernel(case):
+    # hot_threshold = 1: the 1024 largest regions of every batch take the hot path
+    if case == "tb_uniform":
+        lims = [[rl_amd.TB, 50, 60000, 10.0]]
+        tr = trace(21, 300_000, 3_000, 1, 2_000)
+    elif case == "sw_zipf":
+        lims = [[rl_amd.SW, 1000, 60000, 0.0]]
+        tr = trace(22, 300_000, 50_000, 1, 90_000, zipf=1.1, permits_max=1)
+    else:
+        lims = [[rl_amd.SW, 10, 60000, 0.0], [rl_amd.TB, 50, 60000, 10.0],
+                [rl_amd.SW, 5, 1000, 0.0], [rl_amd.TB, 3, 500, 7.0]]
+        tr = trace(23, 300_000, 10_000, len(lims), 200_000, zipf=1.3, ops=0.04, invalid=0.002)
+    got, want, _ = run(lims, tr, batches=3, tune={"hot_threshold": 1})
+    assert_same(got, want, case)
+
+
+def test_hot_two_pass_partition():
+    # > 8192 bins: two partition passes, bin bounds from k_bin_bounds, plus hot regions
+    lims = [[rl_amd.SW, 100, 60000, 0.0], [rl_amd.TB, 50, 60000, 10.0]]
+    tr = hot_trace(15, 1_000_000, 200_000, 0.3, [0, 1], 60_000, hot_keys=4)
+    got, want, e = run(lims, tr, batches=2, capacity=1 << 22, tune={"hot_threshold": 16384})
+    assert_same(got, want, "hot two-pass")
+
+
+def test_hot_stats_and_device_entry():
+    import torch
+    lims = [[rl_amd.SW, 1000, 60000, 0.0]]
+    tr = hot_trace(16, 500_000, 10_000, 0.4, [0], 60_000, permits_max=1)
+    n = len(tr[0])
+    e = rl_amd.Engine(max_batch=n, capacity=1 << 14, stage_timing=True)
+    e.add_limiter(*lims[0])
+    e.tune("hot_threshold", 4096)
+    dev = [torch.from_numpy(np.ascontiguousarray(x)).cuda()
+           for x in (tr[0].view(np.int64), tr[1], tr[2])]
+    allowed = torch.empty(n, dtype=torch.uint8, device="cuda")
+    remaining = torch.empty(n, dtype=torch.int64, device="cuda")
+    e.execute_device(n, *dev, None, None, allowed, remaining)
+    assert e.last_status() == rl_amd.RL_OK
+    want = COracle(lims).run(*tr[:3])
+    assert_same((allowed.cpu().numpy(), remaining.cpu().numpy(), None), want, "device hot")
+    s = e.stats()
+    assert s["allowed"] == int(want[0].sum())
+    assert s["distinct_keys"] == len(np.unique(tr[0]))
+    assert e.stage_times()["region_hot"] > 0

@@ -40,7 +40,7 @@ variants = args.variants.split("/")
 
 
 DEFAULTS = {"ablate": 0, "bin_shift": 0, "upsweep_per_cu": 0, "scatter_per_cu": 0,
-            "unpermute_per_cu": 0}
+            "unpermute_per_cu": 0, "hot_threshold": 16384}
 
 
 def apply(v):

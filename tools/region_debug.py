@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Per-region timeline of the region stage for one bench config (GPU box): which regions
+take longest, how many records/rounds they had, and when they started."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "distributed-rate-limiter_amd", "python"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import rl_amd  # noqa: E402
+from bench import CONFIGS, T0_NS  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="sw_zipf")
+ap.add_argument("--batches", type=int, default=3)
+ap.add_argument("--tune", action="append", default=[])
+args = ap.parse_args()
+cfg = CONFIGS[args.config]
+n = cfg["batch"]
+torch.cuda.set_device(0)
+eng = rl_amd.Engine(device=0, max_batch=n, capacity=cfg["capacity"], stage_timing=True)
+for l in cfg["limiters"]:
+    eng.add_limiter(*l)
+eng.tune("debug_regions", 1)
+for kv in args.tune:
+    k, v = kv.split("=")
+    eng.tune(k, int(v))
+dev = torch.device("cuda", 0)
+keys = torch.empty(n, dtype=torch.int64, device=dev)
+permits = torch.empty(n, dtype=torch.int32, device=dev)
+now = torch.empty(n, dtype=torch.int64, device=dev)
+allowed = torch.empty(n, dtype=torch.uint8, device=dev)
+remaining = torch.empty(n, dtype=torch.int64, device=dev)
+import ctypes  # noqa: E402
+nb = 1 << 24
+for b in range(args.batches):
+    eng.synth_trace(n, keys, permits, now, None, seed=cfg["seed"], n_keys=cfg["n_keys"],
+                    dist=cfg["dist"], zipf_s=cfg.get("zipf_s", 1.1), permits_max=cfg["permits_max"],
+                    t0_ns=T0_NS, span_ns=cfg["span_ns"] * args.batches, index_base=b * n,
+                    n_total=n * args.batches)
+    eng.execute_device(n, keys, permits, now, None, None, allowed, remaining)
+    eng.sync()
+    st = eng.stage_times()
+    d = eng.debug_region_times(nb)
+    d = d[d[:, 1] > 0]
+    t0 = d[:, 0].min()
+    dur = (d[:, 1] - d[:, 0]) / 100.0          # us
+    hot = (d[:, 3] >> np.uint64(63)) == 1
+    rounds = d[:, 3] & np.uint64((1 << 63) - 1)
+    print(f"batch {b}: region stage {st['region']:.2f} ms hot {st['region_hot']:.2f} ms; "
+          f"{len(d)} regions, {hot.sum()} hot; span {(d[:, 1].max() - t0) / 100:.0f} us")
+    order = np.argsort(-dur)[:12]
+    for i in order:
+        print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  recs {int(d[i, 2]):9d} "
+              f"rounds {int(rounds[i]):8d} {'HOT' if hot[i] else ''}")
+    nh = ~hot
+    ends = (d[nh, 1] - t0) / 100
+    for q in (0.5, 0.9, 0.99, 0.999, 1.0):
+        print(f"   normal regions end quantile {q}: {np.quantile(ends, q):9.1f} us")
+    print(f"   normal: sum dur {dur[nh].sum() / 1e3:.1f} ms, recs {int(d[nh, 2].sum())}, "
+          f"rounds {int(rounds[nh].sum())}")
