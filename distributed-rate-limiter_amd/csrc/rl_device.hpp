@@ -315,14 +315,15 @@ __device__ inline int64_t sw_estimate(const SW2& s, const SWGeo& g, int64_t now,
     return d2l(sum);
 }
 
-__device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t permits,
-                                  int64_t now, uint64_t a, uint64_t b, uint64_t c) {
+// sw_step with the request's window geometry precomputed (it depends only on now, w).
+__device__ inline Outcome sw_step_g(const DevLimiter& L, uint32_t op, int32_t permits,
+                                    int64_t now, const SWGeo& geo, uint64_t a, uint64_t b,
+                                    uint64_t c) {
     Outcome o;
     o.mutate = false; o.allowed = false; o.remaining = 0; o.tokens = __builtin_nan("");
     o.a = a; o.b = b; o.c = c;
     const int64_t w = L.window_ms;
     SW2 s = sw_unpack(a, b, c);
-    const SWGeo geo = sw_geo(now, w);
     const int64_t curr_start = geo.curr_start;
     if (op == (uint32_t)kOpReset) {                  // reset (:139-153): DEL curr and prev
         const int64_t prev_start = geo.prev_start;
@@ -359,6 +360,52 @@ __device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t perm
     o.b = (uint64_t)s.b1_cnt | ((uint64_t)s.b0_cnt << 32);
     o.c = (uint64_t)(uint32_t)s.b1_off | ((uint64_t)(uint32_t)s.b0_off << 32);
     return o;
+}
+
+__device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t permits,
+                                  int64_t now, uint64_t a, uint64_t b, uint64_t c) {
+    return sw_step_g(L, op, permits, now, sw_geo(now, L.window_ms), a, b, c);
+}
+
+// Sliding-window acquire at `now` assuming that k earlier requests of the same key, all
+// in now's window and all after the state's newest bucket, were ALLOWED (each INCRs the
+// current bucket by 1, :114-116). Exactly what sw_step returns after those k steps:
+// the current bucket is then curr0 + k (alive: its last INCR is in this window) and the
+// previous bucket is untouched (a roll into this window moves b1 to b0 with its offset).
+struct SWAllow { bool allowed; int64_t remaining; };
+__device__ inline SWAllow sw_try_after_allows(const DevLimiter& L, int32_t permits, int64_t now,
+                                              const SWGeo& g, uint64_t a, uint64_t b, uint64_t c,
+                                              uint32_t k) {
+    const int64_t w = L.window_ms;
+    const SW2 s = sw_unpack(a, b, c);
+    const int64_t curr0 = (s.b1_start == g.curr_start) ? (int64_t)s.b1_cnt : 0;
+    const int64_t prev = sw_get(s, g.prev_start, now, w);
+    const double t = (double)prev * g.prev_weight;            // :174, as sw_estimate
+    const int64_t est = d2l(t + (double)(curr0 + (int64_t)k));
+    SWAllow r;
+    r.allowed = !(est + (int64_t)permits > L.max_permits);
+    const int64_t e2 = r.allowed ? d2l(t + (double)(curr0 + (int64_t)k + 1)) : est;
+    const int64_t rem = L.max_permits - e2;
+    r.remaining = rem > 0 ? rem : 0;
+    return r;
+}
+
+// The state after n such allows, the last at time t_last (the roll of sw_step included).
+__device__ inline void sw_commit_allows(const DevLimiter& L, const SWGeo& g, uint64_t& a,
+                                        uint64_t& b, uint64_t& c, uint32_t n, int64_t t_last) {
+    SW2 s = sw_unpack(a, b, c);
+    if (s.b1_start == g.curr_start) {
+        s.b1_cnt += n;
+    } else {
+        if (s.b1_start == g.curr_start - L.window_ms) { s.b0_cnt = s.b1_cnt; s.b0_off = s.b1_off; }
+        else { s.b0_cnt = 0; s.b0_off = 0; }
+        s.b1_start = g.curr_start;
+        s.b1_cnt = n;
+    }
+    s.b1_off = (int32_t)(t_last - g.curr_start);
+    a = (uint64_t)s.b1_start;
+    b = (uint64_t)s.b1_cnt | ((uint64_t)s.b0_cnt << 32);
+    c = (uint64_t)(uint32_t)s.b1_off | ((uint64_t)(uint32_t)s.b0_off << 32);
 }
 
 // A slot is kept when the region is loaded iff some request at now >= batch_min could

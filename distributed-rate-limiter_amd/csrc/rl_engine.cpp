@@ -23,11 +23,11 @@ namespace {
 
 // Stage timing: events bracket every kernel of a batch; a ring of per-batch event
 // sets is averaged when rl_stage_times is called (no host sync inside a batch).
-constexpr int kMarks = 12;   // marks 0..9 on the engine stream, 10..11 on the hot stream
+constexpr int kMarks = 12;   // marks 0..11 on the engine stream
 constexpr int kStages = 11;
 const char* kStageNames[kStages] = {"upsweep0", "scan0", "scatter0", "upsweep1", "scan1",
                                     "scatter1", "region_offsets", "region", "unpermute", "total",
-                                    "region_hot"};
+                                    "hot_fill"};
 const int kStagePairs[kStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6},
                                      {6, 7}, {7, 8}, {8, 9}, {0, 9}, {10, 11}};
 constexpr int kEvRing = 64;
@@ -52,8 +52,6 @@ struct rl_engine {
     rl_opts opts{};
     int shard_bits = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream_hot = nullptr;       // k_regions_hot runs beside k_regions
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::mutex mu;                          // one batch in flight per engine handle
 
     std::vector<HostLimiter> lims;
@@ -82,7 +80,7 @@ struct rl_engine {
     uint32_t* hot_list = nullptr;           // [kHotMax + 40]: list, k_hot_select's meta, total
     HotInfo* hot_info = nullptr;            // [kHotMax]
     uint64_t* hot_summ = nullptr;           // [hot_summ_cap][4]
-    size_t hot_summ_cap = 0;
+    size_t hot_summ_cap = 0, hot_summ_l1 = 0;
     uint32_t* hot_mark = nullptr;           // [hot_mark_cap] epoch marks per bin
     size_t hot_mark_cap = 0;
     uint32_t epoch = 0;
@@ -176,14 +174,6 @@ extern "C" uint32_t rl_owner_of(uint64_t key_hash, uint16_t, uint32_t shard_coun
     return (uint32_t)(mix64(key_hash) >> (64 - s));
 }
 
-// The hot-region kernel must get its CUs before the (much larger) normal region grid
-// fills the machine, so its stream has the greatest priority the device offers.
-static int hot_priority() {
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
-    return greatest;
-}
-
 extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     if (!out) return RL_E_INVALID_ARG;
     *out = nullptr;
@@ -205,10 +195,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     } else {
         (void)hipGetDevice(&e->device);
     }
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&e->stream_hot, hipStreamNonBlocking, hot_priority()) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         rl_destroy(e);
         return RL_E_DEVICE;
     }
@@ -245,9 +232,6 @@ extern "C" void rl_destroy(rl_engine* e) {
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
     for (int r = 0; r < kEvRing; ++r)
         for (int i = 0; i < kMarks; ++i) if (e->ev[r][i]) (void)hipEventDestroy(e->ev[r][i]);
-    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-    if (e->stream_hot) { (void)hipStreamSynchronize(e->stream_hot); (void)hipStreamDestroy(e->stream_hot); }
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -363,12 +347,15 @@ static int ensure_regions(rl_engine* e, size_t bins) {
     return RL_OK;
 }
 
+// chunk summaries [l1] then group summaries [l1 / 64 + kHotMax + 1], 32 B each
 static int ensure_hot_summ(rl_engine* e, size_t n) {
-    const size_t need = n / kHotChunk + kHotMax + 1;
+    const size_t l1 = n / kHotChunk + kHotMax + 1;
+    const size_t need = l1 + l1 / 64 + kHotMax + 1;
     if (need <= e->hot_summ_cap) return RL_OK;
     dfree(e->hot_summ);
     if (dalloc(&e->hot_summ, need * 4) != RL_OK) { e->hot_summ_cap = 0; return RL_E_NOMEM; }
     e->hot_summ_cap = need;
+    e->hot_summ_l1 = l1;
     return RL_OK;
 }
 
@@ -498,10 +485,10 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
     if (e->debug_regions) {
-        if (e->dbg_cap < (size_t)n_bins * 4) {
+        if (e->dbg_cap < (size_t)n_bins * kDbgWords) {
             dfree(e->dbg);
-            if (dalloc(&e->dbg, (size_t)n_bins * 4) != RL_OK) { e->dbg_cap = 0; return RL_E_NOMEM; }
-            e->dbg_cap = (size_t)n_bins * 4;
+            if (dalloc(&e->dbg, (size_t)n_bins * kDbgWords) != RL_OK) { e->dbg_cap = 0; return RL_E_NOMEM; }
+            e->dbg_cap = (size_t)n_bins * kDbgWords;
         }
         HIP_OK(hipMemsetAsync(e->dbg, 0, e->dbg_cap * sizeof(uint64_t), s));
         ra.dbg = e->dbg;
@@ -513,21 +500,15 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
                                  hot_count, e->hot_mark, e->epoch, s));
         ra.hot_list = e->hot_list; ra.hot_count = hot_count; ra.hot_mark = e->hot_mark;
         ra.epoch = e->epoch;
-        ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ; ra.hot_total = e->hot_list + kHotMax + 36;
+        ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ;
+        ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 4; ra.hot_total = e->hot_list + kHotMax + 36;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
-        HIP_OK(hipEventRecord(e->ev_fork, s));
-        HIP_OK(hipStreamWaitEvent(e->stream_hot, e->ev_fork, 0));
-        mark_on(e, 10, e->stream_hot);
-        HIP_OK(launch_hot_chain(ra, wide, res_bytes, e->stream_hot));
-        mark_on(e, 11, e->stream_hot);
-        HIP_OK(hipEventRecord(e->ev_join, e->stream_hot));
-    } else {
-        mark_on(e, 10, s);
-        mark_on(e, 11, s);
     }
     mark(e, 7);
-    HIP_OK(launch_region(ra, wide, res_bytes, s));
-    if (hot) HIP_OK(hipStreamWaitEvent(s, e->ev_join, 0));
+    HIP_OK(launch_region(ra, wide, res_bytes, s));       // hot chains first, then the regions
+    mark(e, 10);
+    if (hot) HIP_OK(launch_hot_fill(ra, wide, res_bytes, s));
+    mark(e, 11);
     mark(e, 8);
     UnpermArgs ua{};
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
@@ -833,7 +814,7 @@ extern "C" int rl_debug_fetch(rl_engine* e, const char* what, void* out, size_t 
         HIP_OK(hipStreamSynchronize(e->stream));
         const size_t nb = std::min(bytes, e->dbg_cap * sizeof(uint64_t));
         HIP_OK(hipMemcpy(out, e->dbg, nb, hipMemcpyDeviceToHost));
-        return (int)(nb / (4 * sizeof(uint64_t)));
+        return (int)(nb / (kDbgWords * sizeof(uint64_t)));
     }
     return RL_E_INVALID_ARG;
 }

@@ -443,29 +443,84 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         ++n_caperr;
     }
     if (slot >= 0) atomicOr(&S.occ[slot], 2u);
-    // ---- apply in arrival order: per round, the first state-changing request of each
-    // key applies; the key's earlier (non-mutating) requests are final.
+    // ---- apply in arrival order. Per round, two hypotheses about a key's pending requests
+    // are tested at once against its current state: (D) every earlier one is denied (no
+    // state change: SlidingWindowRateLimiter.java:104-111, Lua :61-67) -> the prefix up to
+    // and including the first state-changing request is final; (A, sliding window only)
+    // every earlier one is allowed (the current bucket counts them: :114-116) -> the prefix
+    // up to and including the first denied request is final. The longer prefix is taken,
+    // so a run of denials or a run of allows costs one round, not one per request.
     const bool one_round = (a.ablate & kAblNoRounds) != 0;
     const uint64_t peers = one_round ? (1ULL << lane)
                                      : wave_match((uint32_t)slot, kRegionBits, slot >= 0);
     bool pending = slot >= 0;
+    SWGeo geo{};
+    uint64_t same_w = 0, elig_m = 0;        // (A): lanes in my window / acquires
+    if constexpr (!tb) {
+        if (slot >= 0) geo = sw_geo(q.now_ms, L.window_ms);
+        // window index relative to the wave's first window (2 bits; 3 = "far")
+        int64_t wmin = slot >= 0 ? geo.curr_start : INT64_MAX;
+        for (int o = 32; o > 0; o >>= 1) {
+            const int64_t x = __shfl_xor(wmin, o, 64);
+            wmin = x < wmin ? x : wmin;
+        }
+        int64_t wi = slot >= 0 ? (geo.curr_start - wmin) / L.window_ms : 3;
+        if (wi > 3) wi = 3;
+        const uint64_t b0 = __ballot(wi & 1), b1 = __ballot(wi & 2);
+        same_w = ((wi & 1) ? b0 : ~b0) & ((wi & 2) ? b1 : ~b1);
+        elig_m = __ballot(slot >= 0 && wi < 3 && q.op == (uint32_t)kOpAcquire);
+    }
     while (__any(pending)) {
         ++n_rounds;
         Outcome o{};
+        SWAllow al{false, 0};
+        bool elig = false;
+        const uint64_t pm = __ballot(pending);
+        const uint64_t kp = peers & pm;                        // my key's pending requests
         if (pending) {
+            const uint64_t sa = S.sa[slot], sb = S.sb[slot], sc = S.sc[slot];
             if (a.ablate & kAblNoStep) {
                 o.mutate = (q.permits & 1) != 0; o.allowed = o.mutate; o.remaining = q.permits;
-                o.a = S.sa[slot]; o.b = S.sb[slot]; o.c = S.sc[slot];
+                o.a = sa; o.b = sb; o.c = sc;
             } else {
-                if constexpr (tb)
-                    o = tb_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot]);
-                else
-                    o = sw_step(L, q.op, q.permits, q.now_ms, S.sa[slot], S.sb[slot], S.sc[slot]);
+                if constexpr (tb) {
+                    o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
+                } else {
+                    o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc);
+                    // (A) needs: all pending peers acquires in one window, not before the
+                    // newest bucket, and more than one of them
+                    elig = (kp & ~(elig_m & same_w)) == 0 && (kp & (kp - 1)) != 0 &&
+                           (int64_t)sa <= geo.curr_start;
+                    if (elig) al = sw_try_after_allows(L, q.permits, q.now_ms, geo, sa, sb, sc,
+                                                       popc_below(kp));
+                }
             }
         }
         const uint64_t mut = __ballot(pending && o.mutate) & peers;
         const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
-        if (pending && lane <= fm) {
+        bool use_a = false;
+        uint32_t fa = 64u;
+        if constexpr (!tb) {
+            const uint64_t den = __ballot(pending && elig && !al.allowed) & peers;
+            fa = den ? (uint32_t)__builtin_ctzll(den) : 64u;
+            use_a = elig && fa > fm;             // the allow hypothesis decides more
+        }
+        if (pending && use_a) {
+            if constexpr (!tb) {
+                if (lane <= fa) {
+                    const uint64_t ok = kp & (fa >= 64u ? ~0ULL : ((1ULL << fa) - 1));   // the allows
+                    if (ok && lane == 63u - (uint32_t)__builtin_clzll(ok)) {   // the last allow commits
+                        uint64_t na = S.sa[slot], nb = S.sb[slot], nc = S.sc[slot];
+                        sw_commit_allows(L, geo, na, nb, nc, (uint32_t)__popcll(ok), q.now_ms);
+                        S.sa[slot] = na; S.sb[slot] = nb; S.sc[slot] = nc;
+                    }
+                    r.out = pack_result(al.allowed, al.remaining);
+                    r.tok = __builtin_nan("");
+                    n_allowed += al.allowed ? 1u : 0u;
+                    pending = false;
+                }
+            }
+        } else if (pending && lane <= fm) {
             if (lane == fm) { S.sa[slot] = o.a; S.sb[slot] = o.b; S.sc[slot] = o.c; }
             r.out = pack_result(o.allowed, o.remaining);
             r.tok = o.tokens;
@@ -477,25 +532,23 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
     return r;
 }
 
-template <class Codec, class Res, bool TOK, int BS>
-__global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
+template <class Codec, class Res, bool TOK, int BS, class LdsT>
+__device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
     constexpr uint32_t RPB = 1u << BS;              // regions per bin
-    __shared__ RegionLds<Codec, (RPB > 1)> S;
 
     // RPB = 8: block g = 64q + 8r + x  ->  bin 8q + x, region r of that bin (see above)
-    const uint32_t g = blockIdx.x;
     const uint32_t bin = RPB == 1 ? g : (g / 64) * 8 + (g % 8);
     const uint32_t rb = RPB == 1 ? 0u : (g / 8) % 8;
     const uint32_t n_bins = a.n_regions / RPB;
     if (bin >= n_bins) return;
-    if (a.hot_mark && a.hot_mark[bin] == a.epoch) return;     // owned by k_regions_hot
+    if (a.hot_mark && a.hot_mark[bin] == a.epoch) return;     // owned by hot_chain
     const uint32_t start = a.rstart[bin];
     const uint32_t cnt = a.rend ? a.rend[bin] - start : a.rcount[bin];
     if (cnt == 0) return;
     const uint32_t end = start + cnt;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t region = bin * RPB + rb;
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
@@ -634,7 +687,7 @@ __global__ __launch_bounds__(64) void k_regions(RegionArgs a) {
         atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
         atomicAdd(&a.ctl->regions, 1ULL);
         if (a.dbg) {
-            uint64_t* d = a.dbg + (size_t)bin * 4;
+            uint64_t* d = a.dbg + (size_t)bin * kDbgWords;
             d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = cnt; d[3] = n_rounds;
         }
     }
@@ -767,6 +820,9 @@ __global__ __launch_bounds__(64) void k_hot_prep(RegionArgs a) {
         f.n_chunks = (end - start + kHotChunk - 1) / kHotChunk;
         f.chunk_base = 0;
         f.ok = (key >> 6) >= 2u ? 1u : 0u;
+        f.n_groups = (f.n_chunks + 63) / 64;
+        f.group_base = 0;
+        f.pad[0] = f.pad[1] = 0;
         a.hot_info[i] = f;
     }
 }
@@ -776,22 +832,68 @@ __global__ __launch_bounds__(1024) void k_hot_scan(RegionArgs a) {
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     const uint32_t t = threadIdx.x;
     const uint32_t v = t < hc ? a.hot_info[t].n_chunks : 0u;
-    uint32_t tot;
+    uint32_t tot, tot2;
     const uint32_t ex = block_exclusive_scan<1024>(v, tmp, &tot);
-    if (t < hc) a.hot_info[t].chunk_base = ex;
-    if (t == 0) *a.hot_total = tot;
+    const uint32_t v2 = t < hc ? a.hot_info[t].n_groups : 0u;
+    const uint32_t ex2 = block_exclusive_scan<1024>(v2, tmp, &tot2);
+    if (t < hc) {
+        a.hot_info[t].chunk_base = ex;
+        a.hot_info[t].group_base = ex2;
+    }
+    if (t == 0) { a.hot_total[0] = tot; a.hot_total[1] = tot2; }
 }
 
-// Phase A (one wave per 64-record chunk, all CUs): what the chain needs to decide a chunk
-// without reading it: the time range of the hot key's plain acquires, and how many
-// records need the exact path (other keys, invalid, peek / reset of the hot key).
-// Summary words: [0] min now, [1] max now, [2] n_special | n_hot << 8 | n_early << 16,
-// [3] verdict (k_hot_chain: 1 = decided by the thresholds, words 0-2 then hold the state).
+// Phase A2 (one wave per 64 chunks): the same summary over 4096 records, so the chain
+// decides the long runs of a hot key's denials 4096 records per test.
+__global__ __launch_bounds__(256) void k_hot_summ2(RegionArgs a) {
+    __shared__ uint32_t s_base[kHotMax + 1];
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    const uint32_t total = a.hot_total[1];
+    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].group_base;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t g = blockIdx.x * 4 + wid; g < total; g += gridDim.x * 4) {
+        const uint32_t i = hot_region_of(s_base, hc, g);
+        const HotInfo f = a.hot_info[i];
+        const uint32_t c = (g - s_base[i]) * 64 + lane;
+        uint64_t mn = ~0ULL, mx = 0;
+        uint32_t w = 0;
+        if (c < f.n_chunks) {
+            const uint64_t* d = a.hot_summ + (size_t)(f.chunk_base + c) * 4;
+            mn = ord_key((int64_t)d[0]);
+            mx = ord_key((int64_t)d[1]);
+            w = (uint32_t)d[2];
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t x = __shfl_xor(mn, o, 64), y = __shfl_xor(mx, o, 64);
+            mn = x < mn ? x : mn;
+            mx = y > mx ? y : mx;
+        }
+        const uint32_t ns = __ballot((w & 0xFFu) != 0) ? 1u : 0u;       // flags, not counts
+        const uint32_t nh = __ballot(((w >> 8) & 0xFFu) != 0) ? 1u : 0u;
+        const uint32_t ne = __ballot(((w >> 16) & 0xFFu) != 0) ? 1u : 0u;
+        const uint32_t no = __ballot(((w >> 24) & 0xFFu) != 0) ? 1u : 0u;
+        if (lane == 0) {
+            uint64_t* d = a.hot_summ2 + (size_t)g * 4;
+            d[0] = mn ^ 0x8000000000000000ULL;
+            d[1] = mx ^ 0x8000000000000000ULL;
+            d[2] = ns | (nh << 8) | (ne << 16);
+            d[3] = (uint64_t)no << 8;                   // other keys: kept through the verdict
+        }
+    }
+}
+
+// Phase A (one wave per 64-record chunk, all CUs): what the chain needs to decide the hot
+// key's records of a chunk without reading it: the time range of its plain acquires, and
+// how many of its records need the exact path (peek / reset). Summary words: [0] min now,
+// [1] max now, [2] n_special | n_hot << 8 | n_early << 16 | n_other << 24, [3] verdict:
+// bit 0 = hot records decided by the thresholds (words 0-2 then hold the key's state),
+// bit 1 = TB early rejects among them, bits 8-15 = records of other keys.
 template <class Codec>
 __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
     __shared__ uint32_t s_base[kHotMax + 1];
     const uint32_t hc = min(a.hot_count[0], kHotMax);
-    const uint32_t total = *a.hot_total;
+    const uint32_t total = a.hot_total[0];
     for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].chunk_base;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -809,7 +911,8 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
         const bool acq = q.op == (uint32_t)kOpAcquire;
         const bool early = hot && acq && L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
         const bool plain = hot && acq && !early;
-        const bool special = valid && !(hot && acq);
+        const bool special = hot && !acq;                 // the hot key's peek / reset
+        const bool other = valid && !hot;                 // every other key (and invalid)
         uint64_t mn = plain ? ord_key(q.now_ms) : ~0ULL, mx = plain ? ord_key(q.now_ms) : 0ULL;
         for (int o = 32; o > 0; o >>= 1) {
             const uint64_t x = __shfl_xor(mn, o, 64), y = __shfl_xor(mx, o, 64);
@@ -819,30 +922,38 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
         const uint32_t ns = (uint32_t)__popcll(__ballot(special));
         const uint32_t nh = (uint32_t)__popcll(__ballot(hot));
         const uint32_t ne = (uint32_t)__popcll(__ballot(early));
+        const uint32_t no = (uint32_t)__popcll(__ballot(other));
         if (lane == 0) {
             uint64_t* d = a.hot_summ + (size_t)g * 4;
             d[0] = mn == ~0ULL ? (uint64_t)INT64_MAX : (mn ^ 0x8000000000000000ULL);
             d[1] = mx == 0ULL ? (uint64_t)INT64_MIN : (mx ^ 0x8000000000000000ULL);
-            d[2] = ns | (nh << 8) | (ne << 16);
-            d[3] = 0;
+            d[2] = ns | (nh << 8) | (ne << 16) | (no << 24);
+            d[3] = (uint64_t)no << 8;
         }
     }
 }
 
-// Phase B (one wave per listed region, beside k_regions): walks the region's chunk
-// summaries in arrival order with the hot key's threshold pair; a chunk whose hot-key
-// times all lie in [T0, T1) and that holds nothing else is decided without being read
-// (its verdict + the key's state go back into the summary for k_hot_fill). Any other
-// chunk is processed here record by record: the hot key through the fast check and the
-// wavefront-per-key sequential run, the other keys through wave_apply.
+// Phase B (one 2-wave workgroup per listed region, beside k_regions). Wave 0 (pass 1)
+// walks the region's summaries in arrival order with the hot key's threshold pair: a
+// group of 64 chunks, or a chunk, whose hot-key times all lie in [T0, T1) has its hot
+// records decided without being read (verdict + the key's state go back into the summary
+// for k_hot_fill); any other chunk has its hot records processed one by one (fast check,
+// then the wavefront-per-key sequential run). Wave 1 (pass 2), at the same time, applies
+// every other key of the region in arrival order, 64 records at a time through
+// wave_apply. The passes touch disjoint slots of the shared LDS table (wave 0 only the
+// hot key's state, wave 1 never that slot), so they need no synchronisation.
+// Runs as the first kHotMax workgroups of k_regions<..., HOT = true>, so the chains are
+// dispatched before the normal regions fill the machine.
 template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(64) void k_hot_chain(RegionArgs a) {
+__device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Codec, true>& S) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
-    __shared__ RegionTable S;
+    __shared__ int32_t s_hslot;
     const uint32_t hc = min(a.hot_count[0], kHotMax);
-    const uint32_t i = blockIdx.x, lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (i >= hc) return;
+    // the passes are sequential critical paths beside thousands of normal-region waves
+    __builtin_amdgcn_s_setprio(3);
     const HotInfo f = a.hot_info[i];
     const uint32_t region = f.bin;                    // bin_shift 0: bin == region
     const DevLimiter L = a.lims[a.region_lim[region]];
@@ -853,66 +964,83 @@ __global__ __launch_bounds__(64) void k_hot_chain(RegionArgs a) {
     Res* res = (Res*)a.res;
     const uint32_t pad = a.n_total + lane;
     if (a.ctl->span_overflow != 0) {                  // whole batch rejected (see k_regions)
-        for (uint32_t j = f.start + lane; j < f.end; j += 64) {
+        for (uint32_t j = f.start + threadIdx.x; j < f.end; j += 128) {
             res[j] = (Res)pack_result(false, kRemInvalid);
             if (TOK) a.tok[j] = __builtin_nan("");
         }
         return;
     }
     const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    // ---- load + rebuild the region (as k_regions), find or insert the hot key's slot
     Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
-    Slot img[NS / 64];
+    if (wid == 0) {
+        // ---- load + rebuild the region (as k_regions), find or insert the hot key's slot
+        Slot img[NS / 64];
 #pragma unroll
-    for (uint32_t k = 0; k < NS / 64; ++k) {
-        S.occ[lane + 64 * k] = 0;
-        img[k] = tab[lane + 64 * k];
-    }
-    wave_fence();
+        for (uint32_t k = 0; k < NS / 64; ++k) {
+            S.occ[lane + 64 * k] = 0;
+            img[k] = tab[lane + 64 * k];
+        }
+        wave_fence();
 #pragma unroll
-    for (uint32_t k = 0; k < NS / 64; ++k) {
-        const Slot v = img[k];
-        if (slot_live(L, v, lo)) {
-            uint32_t p = slot_home(v.tag);
-            while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
-            S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
+        for (uint32_t k = 0; k < NS / 64; ++k) {
+            const Slot v = img[k];
+            if (slot_live(L, v, lo)) {
+                uint32_t p = slot_home(v.tag);
+                while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+                S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
+            }
         }
-    }
-    wave_fence();
-    int32_t hslot = -1;
-    if (f.ok) {
-        const uint32_t p0 = slot_home(f.tag);
-        for (uint32_t k = 0; k < NS; ++k) {                 // linear probing, as the rebuild
-            const uint32_t p = (p0 + k) & (NS - 1);
-            const uint32_t o = S.occ[p];
-            if (!(o & 1u) || S.tag[p] == f.tag) { hslot = (int32_t)p; break; }
-        }
-        if (hslot >= 0 && !(S.occ[hslot] & 1u)) {
-            wave_fence();
-            if (lane == 0) {
+        wave_fence();
+        int32_t hslot = -1;
+        if (f.ok) {
+            const uint32_t p0 = slot_home(f.tag);
+            for (uint32_t k = 0; k < NS; ++k) {             // linear probing, as the rebuild
+                const uint32_t p = (p0 + k) & (NS - 1);
+                const uint32_t o = S.occ[p];
+                if (!(o & 1u) || S.tag[p] == f.tag) { hslot = (int32_t)p; break; }
+            }
+            if (hslot >= 0 && !(S.occ[hslot] & 1u) && lane == 0) {
                 S.occ[hslot] = 1u; S.tag[hslot] = f.tag; S.sa[hslot] = 0; S.sb[hslot] = 0; S.sc[hslot] = 0;
             }
-            wave_fence();
         }
+        if (lane == 0) s_hslot = hslot;
     }
+    __syncthreads();
+    // hot_ok false (no dominant key, or its region is full): pass 2 takes every record
+    const int32_t hslot = s_hslot;
     const bool hot_ok = hslot >= 0;
     const uint32_t hs = hot_ok ? (uint32_t)hslot : 0u;
     const uint64_t tag = f.tag;
+    auto is_hot = [&](const Req& q, bool valid) { return hot_ok && valid && !q.invalid && q.h == tag; };
+    auto summ_at = [&](uint32_t c) {
+        return a.hot_summ + (size_t)(f.chunk_base + (c < f.n_chunks ? c : 0)) * 4;
+    };
+    auto grp_at = [&](uint32_t g) {
+        return a.hot_summ2 + (size_t)(f.group_base + (g < f.n_groups ? g : 0)) * 4;
+    };
 
-    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0;
+    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0, n_other = 0;
+    uint64_t cyc_run = 0, cyc_search = 0, cyc_detail = 0, cyc_pass2 = 0;   // debug stamps
     bool any_hot = false;
-    auto body = [&](auto algo) {
+    auto pass1 = [&](auto algo) {
         constexpr int A = decltype(algo)::value;
         int64_t T0 = lo, T1 = lo;                         // empty range until computed
-        if (hot_ok) hot_thresholds<A>(L, S.sa[hs], S.sb[hs], S.sc[hs], lo, lo, hi, lane, &T0, &T1);
-        // one chunk, record by record (lane = arrival order inside the chunk)
+        hot_thresholds<A>(L, S.sa[hs], S.sb[hs], S.sc[hs], lo, lo, hi, lane, &T0, &T1);
+        // the hot records of one chunk, one by one (lane = arrival order inside the chunk).
+        // The next chunk's records are prefetched: undecided chunks come in runs (an allow,
+        // then the request that finds the key at its limit again).
+        Rec pre = recs[min(f.start + lane, f.end - 1)];
+        uint32_t pre_c = 0;
         auto detail = [&](uint32_t c) {
             ++n_detail;
+            const uint64_t c_det = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t j = f.start + c * kHotChunk + lane;
             const bool valid = j < f.end;
-            const Rec r = recs[valid ? j : f.start];
+            const Rec r = pre_c == c ? pre : recs[valid ? j : f.start];
+            pre_c = c + 1;
+            pre = recs[min(f.start + pre_c * kHotChunk + lane, f.end - 1)];
             const Req q = Codec::dec(r, base);
-            const bool hot = hot_ok && valid && !q.invalid && q.h == tag;
+            const bool hot = is_hot(q, valid);
             uint64_t out = 0;
             double tk = __builtin_nan("");
             bool pend = hot;
@@ -931,6 +1059,7 @@ __global__ __launch_bounds__(64) void k_hot_chain(RegionArgs a) {
                 }
                 if (first == 64u) break;
                 // sequential run from `first`, state in registers, until a (deny, 0)
+                const uint64_t c_run = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
                 const uint64_t pm = __ballot(pend);
                 uint64_t sa = S.sa[hs], sb = S.sb[hs], sc = S.sc[hs];
                 uint32_t flag = 0;
@@ -943,7 +1072,7 @@ __global__ __launch_bounds__(64) void k_hot_chain(RegionArgs a) {
                     Outcome o;
                     if constexpr (A == kAlgoTB) o = tb_step(L, op, pj, now, sa, sb, sc);
                     else o = sw_step(L, op, pj, now, sa, sb, sc);
-                    if (o.mutate) { sa = o.a; sb = o.b; sc = o.c; flag |= 1u; }
+                    if (o.mutate) { sa = o.a; sb = o.b; sc = o.c; flag |= 1u; from = now; }
                     if (lane == jj) { out = pack_result(o.allowed, o.remaining); tk = o.tokens; pend = false; }
                     if (lane == 0 && o.allowed) ++n_allowed;
                     if (!o.mutate && !o.allowed && o.remaining == 0 && op == (uint32_t)kOpAcquire) {
@@ -955,53 +1084,167 @@ __global__ __launch_bounds__(64) void k_hot_chain(RegionArgs a) {
                 wave_fence();
                 if (lane == 0) { S.sa[hs] = sa; S.sb[hs] = sb; S.sc[hs] = sc; }
                 wave_fence();
-                if (flag & 2u) hot_thresholds<A>(L, sa, sb, sc, from, lo, hi, lane, &T0, &T1);
-                else if (flag & 1u) T1 = T0;              // changed state: no fast range yet
+                // (deny, 0) at `from`, or the run ended after a state change at `from`:
+                // search T1 from there (an empty range if the key is below its limit)
+                const uint64_t c_srch = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                if (flag) hot_thresholds<A>(L, sa, sb, sc, from, lo, hi, lane, &T0, &T1);
+                if (a.dbg) {
+                    const uint64_t c_end = __builtin_amdgcn_s_memtime();
+                    cyc_run += c_srch - c_run;
+                    cyc_search += c_end - c_srch;
+                }
             }
-            const bool nonhot = valid && !hot;
-            if (__any(nonhot)) {                          // every other key of the region
-                const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, nonhot, j, base, pad,
-                                                        n_allowed, n_invalid, n_caperr, n_rounds);
-                if (nonhot) { out = ap.out; tk = ap.tok; }
-            }
-            if (valid) {
+            if (hot) {
                 res[j] = (Res)out;
                 if (TOK) a.tok[j] = tk;
             }
+            if (a.dbg) cyc_detail += __builtin_amdgcn_s_memtime() - c_det;
         };
-        for (uint32_t c0 = 0; c0 < f.n_chunks; c0 += 64) {
-            const uint32_t c = c0 + lane;
+        // level 1: the chunks of one group of 64
+        auto walk_group = [&](uint32_t grp) {
+            const uint32_t c = grp * 64 + lane;
             const bool has = c < f.n_chunks;
-            uint64_t* sm = a.hot_summ + (size_t)(f.chunk_base + (has ? c : 0)) * 4;
+            uint64_t* sm = summ_at(c);
+            const ulonglong2 v01 = *(const ulonglong2*)sm;
+            const uint64_t v2 = sm[2];
             int64_t mn = INT64_MAX, mx = INT64_MIN;
-            uint32_t ns = 0, ne = 0;
+            uint32_t ns = 0, ne = 0, nh = 0;
             if (has) {
-                mn = (int64_t)sm[0];
-                mx = (int64_t)sm[1];
-                const uint32_t w = (uint32_t)sm[2];
+                mn = (int64_t)v01.x;
+                mx = (int64_t)v01.y;
+                const uint32_t w = (uint32_t)v2;
                 ns = w & 0xFFu;
+                nh = (w >> 8) & 0xFFu;
                 ne = (w >> 16) & 0xFFu;
-                any_hot |= ((w >> 8) & 0xFFu) != 0;
+                any_hot |= nh != 0;
             }
-            uint64_t todo = __ballot(has);
+            uint64_t todo = __ballot(has && nh != 0);
             while (todo) {
                 const bool skip = ns == 0 && mn >= T0 && mx < T1;
                 const uint64_t nsk = todo & ~__ballot(skip);
                 const uint32_t fst = nsk ? (uint32_t)__builtin_ctzll(nsk) : 64u;
-                if (((todo >> lane) & 1u) && lane < fst) {      // decided: state is constant here
-                    sm[0] = S.sa[hs]; sm[1] = S.sb[hs]; sm[2] = S.sc[hs]; sm[3] = ne ? 3u : 1u;
+                if (((todo >> lane) & 1u) && lane < fst) {  // decided: the key's state is constant here
+                    sm[0] = S.sa[hs]; sm[1] = S.sb[hs]; sm[2] = S.sc[hs];
+                    sm[3] = (((v2 >> 24) & 0xFFu) << 8) | (ne ? 3u : 1u);
                 }
                 if (fst == 64u) break;
                 todo &= fst == 63u ? 0ULL : ~((2ULL << fst) - 1);
-                detail(c0 + fst);
+                detail(grp * 64 + fst);
+            }
+        };
+        // level 2: 64 groups per test, the next 64 in flight
+        ulonglong2 nx01 = *(const ulonglong2*)grp_at(lane);
+        uint64_t nx2 = grp_at(lane)[2], nx3 = grp_at(lane)[3];
+        for (uint32_t g0 = 0; g0 < f.n_groups; g0 += 64) {
+            const uint32_t g = g0 + lane;
+            const bool has = g < f.n_groups;
+            uint64_t* sg = grp_at(g);
+            const ulonglong2 v01 = nx01;
+            const uint64_t v2 = nx2, v3 = nx3;
+            nx01 = *(const ulonglong2*)grp_at(g + 64);
+            nx2 = grp_at(g + 64)[2];
+            nx3 = grp_at(g + 64)[3];
+            const int64_t mn = (int64_t)v01.x, mx = (int64_t)v01.y;
+            const uint32_t w = (uint32_t)v2;
+            const bool ns = (w & 0xFFu) != 0, nh = ((w >> 8) & 0xFFu) != 0, ne = ((w >> 16) & 0xFFu) != 0;
+            any_hot |= has && nh;
+            uint64_t todo = __ballot(has && nh);
+            while (todo) {
+                const bool skip = !ns && mn >= T0 && mx < T1;
+                const uint64_t nsk = todo & ~__ballot(skip);
+                const uint32_t fst = nsk ? (uint32_t)__builtin_ctzll(nsk) : 64u;
+                if (((todo >> lane) & 1u) && lane < fst) {  // a whole group decided
+                    sg[0] = S.sa[hs]; sg[1] = S.sb[hs]; sg[2] = S.sc[hs];
+                    sg[3] = (v3 & 0xFF00u) | (ne ? 3u : 1u);
+                }
+                if (fst == 64u) break;
+                todo &= fst == 63u ? 0ULL : ~((2ULL << fst) - 1);
+                walk_group(g0 + fst);
             }
         }
     };
-    if (L.algo == kAlgoTB) body(std::integral_constant<int, kAlgoTB>{});
-    else body(std::integral_constant<int, kAlgoSW>{});
+    auto pass2 = [&](auto algo) {
+        constexpr int A = decltype(algo)::value;
+        const uint64_t c_p2 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+        uint32_t head = 0, count = 0;                     // LDS ring (wave-uniform)
+        auto apply64 = [&](uint32_t valid_n) {
+            const bool v = lane < valid_n;
+            const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
+            const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
+                                                    pad, n_allowed, n_invalid, n_caperr, n_rounds);
+            if (v) {
+                res[ap.j] = (Res)ap.out;
+                if (TOK) a.tok[ap.j] = ap.tok;
+            }
+        };
+        auto take = [&](const Rec& r, uint32_t j, bool valid) {   // append other keys' records
+            const bool other = valid && !is_hot(Codec::dec(r, base), valid);
+            const uint64_t bal = __ballot(other);
+            if (other) {
+                const uint32_t k = (head + count + popc_below(bal)) % kRing;
+                S.ring[k] = r;
+                S.ring_pos[k] = j;
+            }
+            count += (uint32_t)__popcll(bal);
+            n_other += lane == 0 ? (uint32_t)__popcll(bal) : 0u;
+            wave_fence();
+            if (count >= 64) {
+                apply64(64);
+                head = (head + 64) % kRing;
+                count -= 64;
+            }
+        };
+        for (uint32_t g0 = 0; g0 < f.n_groups; g0 += 64) {
+            const uint32_t g = g0 + lane;
+            const bool gho = g < f.n_groups && (!hot_ok || ((grp_at(g)[3] >> 8) & 1u));
+            uint64_t gtodo = __ballot(gho);
+            while (gtodo) {
+                const uint32_t grp = g0 + (uint32_t)__builtin_ctzll(gtodo);
+                gtodo &= gtodo - 1;
+                const uint32_t c = grp * 64 + lane;
+                uint32_t no = 0;
+                if (c < f.n_chunks) no = hot_ok ? (uint32_t)(summ_at(c)[3] >> 8) & 0xFFu : 64u;
+                uint64_t todo = __ballot(no != 0);
+                // the chunks with other keys' records, the next one's records in flight
+                auto rec_of = [&](uint32_t cc) { return recs[min(f.start + cc * kHotChunk + lane, f.end - 1)]; };
+                Rec nxt = todo ? rec_of(grp * 64 + (uint32_t)__builtin_ctzll(todo)) : Rec{};
+                while (todo) {
+                    const uint32_t cc = grp * 64 + (uint32_t)__builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const Rec r = nxt;
+                    if (todo) nxt = rec_of(grp * 64 + (uint32_t)__builtin_ctzll(todo));
+                    const uint32_t j = f.start + cc * kHotChunk + lane;
+                    take(r, j, j < f.end);
+                }
+            }
+        }
+        if (count > 0) apply64(count);
+        if (a.dbg) cyc_pass2 += __builtin_amdgcn_s_memtime() - c_p2;
+    };
+    if (wid == 0) {
+        if (hot_ok) {
+            if (L.algo == kAlgoTB) pass1(std::integral_constant<int, kAlgoTB>{});
+            else pass1(std::integral_constant<int, kAlgoSW>{});
+        }
+    } else {
+        if (L.algo == kAlgoTB) pass2(std::integral_constant<int, kAlgoTB>{});
+        else pass2(std::integral_constant<int, kAlgoSW>{});
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        n_allowed += __shfl_xor(n_allowed, off, 64);
+        n_invalid += __shfl_xor(n_invalid, off, 64);
+        n_caperr += __shfl_xor(n_caperr, off, 64);
+    }
+    if (lane == 0) {
+        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
+        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
+        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
+    }
     // ---- write the region back, statistics
-    const bool touched_hot = __any(any_hot);
-    wave_fence();
+    __shared__ uint64_t s_w1[2];                      // wave 1's debug counters
+    if (wid == 1 && lane == 0) { s_w1[0] = n_other; s_w1[1] = cyc_pass2; }
+    const bool touched_hot = __syncthreads_or(any_hot);
+    if (wid != 0) return;
     if (lane == 0 && hot_ok && touched_hot) S.occ[hs] |= 2u;
     wave_fence();
     uint32_t touched = 0;
@@ -1013,23 +1256,36 @@ __global__ __launch_bounds__(64) void k_hot_chain(RegionArgs a) {
         tab[sl] = v;
         touched += (o >> 1) & 1u;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        n_allowed += __shfl_xor(n_allowed, off, 64);
-        n_invalid += __shfl_xor(n_invalid, off, 64);
-        n_caperr += __shfl_xor(n_caperr, off, 64);
-        touched += __shfl_xor(touched, off, 64);
-    }
+    for (int off = 32; off > 0; off >>= 1) touched += __shfl_xor(touched, off, 64);
     if (lane == 0) {
-        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
-        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
-        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
         atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
         atomicAdd(&a.ctl->regions, 1ULL);
         if (a.dbg) {
-            uint64_t* d = a.dbg + (size_t)region * 4;
+            uint64_t* d = a.dbg + (size_t)region * kDbgWords;
+            // top bit: a hot region; bits 0-31: detailed chunks, 32-62: other-key records
             d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = f.end - f.start;
-            d[3] = (uint64_t)n_detail | (1ULL << 63);     // top bit: a hot region; low: detailed chunks
+            d[3] = (uint64_t)n_detail | (s_w1[0] << 32) | (1ULL << 63);
+            d[4] = cyc_detail; d[5] = cyc_run; d[6] = cyc_search; d[7] = s_w1[1];
         }
+    }
+}
+
+// HOT: 2-wave workgroups; the first kHotMax run the hot regions' chains (hot_chain), the
+// rest two normal regions each: one launch, so the chains are dispatched before the
+// normal regions fill the machine, at the LDS per wave of the plain kernel.
+template <class Codec, class Res, bool TOK, int BS, bool HOT>
+__global__ __launch_bounds__(HOT ? 128 : 64, HOT ? 4 : 1) void k_regions(RegionArgs a) {
+    if constexpr (HOT) {
+        __shared__ union U { RegionTable two[2]; RegionLds<Codec, true> one; } S;
+        if (blockIdx.x < kHotMax) {
+            hot_chain<Codec, Res, TOK>(a, blockIdx.x, S.one);
+            return;
+        }
+        region_body_t<Codec, Res, TOK, BS>(a, (blockIdx.x - kHotMax) * 2 + (threadIdx.x >> 6),
+                                           S.two[threadIdx.x >> 6]);
+    } else {
+        __shared__ RegionLds<Codec, (BS > 0)> S;
+        region_body_t<Codec, Res, TOK, BS>(a, blockIdx.x, S);
     }
 }
 
@@ -1038,7 +1294,7 @@ template <class Codec, class Res, bool TOK>
 __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
     __shared__ uint32_t s_base[kHotMax + 1];
     const uint32_t hc = min(a.hot_count[0], kHotMax);
-    const uint32_t total = *a.hot_total;
+    const uint32_t total = a.hot_total[0];
     for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].chunk_base;
     __syncthreads();
     if (a.ctl->span_overflow != 0) return;
@@ -1047,20 +1303,28 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
     const int64_t base = a.ctl->base_ms;
     Res* res = (Res*)a.res;
     for (uint32_t g = blockIdx.x * 4 + wid; g < total; g += gridDim.x * 4) {
-        const uint64_t* sm = a.hot_summ + (size_t)g * 4;
-        if (!(sm[3] & 1u)) continue;
         const uint32_t i = hot_region_of(s_base, hc, g);
         const HotInfo f = a.hot_info[i];
-        const uint32_t j = f.start + (g - s_base[i]) * kHotChunk + lane;
+        const uint32_t c = g - s_base[i];
+        const uint64_t* s1 = a.hot_summ + (size_t)g * 4;
+        const uint64_t* s2 = a.hot_summ2 + (size_t)(f.group_base + c / 64) * 4;
+        const uint64_t v2 = s2[3], v1 = s1[3];
+        // decided as part of its group (state in the group summary), or on its own
+        const uint64_t* sm = (v2 & 1u) ? s2 : s1;
+        const uint64_t verdict = (v2 & 1u) ? ((v2 & 3u) | (v1 & 0xFF00u)) : v1;
+        if (!(verdict & 1u)) continue;
+        const uint32_t j = f.start + c * kHotChunk + lane;
         if (j >= f.end) continue;
-        // every record here is the hot key's acquire (n_special == 0); TB permits > max
-        // (verdict bit 1) are the only ones not (deny, 0)
+        // the hot records here are acquires (n_special == 0); TB permits > max (verdict
+        // bit 1) are the only ones not (deny, 0); other keys' records (bits 8-15) are
+        // k_hot_chain's
         const DevLimiter& L = a.lims[a.region_lim[f.bin]];
-        if (!TOK && !(sm[3] & 2u)) {
+        if (!TOK && !(verdict & 0xFF02u)) {
             res[j] = (Res)pack_result(false, 0);
             continue;
         }
         const Req q = Codec::dec(recs[j], base);
+        if (q.invalid || q.h != f.tag) continue;          // another key (f.ok holds here)
         const bool early = L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
         res[j] = (Res)pack_result(false, early ? kRemUnknown : 0);
         if (TOK) a.tok[j] = (L.algo == kAlgoTB && !early) ? tb_refill(L, q.now_ms, sm[0], sm[1], sm[2])
@@ -1442,15 +1706,19 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
 template <class Codec, class Res>
 static void region_launch(const RegionArgs& a, hipStream_t s) {
     const dim3 b(64);
-    if (a.bin_shift == 0) {
+    if (a.bin_shift == 0 && a.hot_mark) {                // hot chains + normal regions
+        const dim3 g(kHotMax + (a.n_regions + 1) / 2), b2(128);
+        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0, true>), g, b2, 0, s, a);
+        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0, true>), g, b2, 0, s, a);
+    } else if (a.bin_shift == 0) {
         const dim3 g(a.n_regions);
-        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0>), g, b, 0, s, a);
-        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0>), g, b, 0, s, a);
+        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0, false>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0, false>), g, b, 0, s, a);
     } else {
         const uint32_t n_bins = a.n_regions / kRegionsPerBin;
         const dim3 g((n_bins + 7) / 8 * 64);
-        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 3>), g, b, 0, s, a);
-        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 3>), g, b, 0, s, a);
+        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 3, false>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 3, false>), g, b, 0, s, a);
     }
 }
 
@@ -1469,26 +1737,22 @@ hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s) {
     hipLaunchKernelGGL(k_hot_scan, dim3(1), dim3(1024), 0, s, a);
     if (wide) hipLaunchKernelGGL(k_hot_summ<CodecW>, gp, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_hot_summ<CodecC>, gp, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hot_summ2, gp, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 template <class Codec, class Res>
-static void hot_chain_launch(const RegionArgs& a, hipStream_t s) {
+static void hot_fill_launch(const RegionArgs& a, hipStream_t s) {
     const dim3 gp(persistent_grid(1u << 30, 4));
-    if (a.tok) {
-        hipLaunchKernelGGL((k_hot_chain<Codec, Res, true>), dim3(kHotMax), dim3(64), 0, s, a);
-        hipLaunchKernelGGL((k_hot_fill<Codec, Res, true>), gp, dim3(256), 0, s, a);
-    } else {
-        hipLaunchKernelGGL((k_hot_chain<Codec, Res, false>), dim3(kHotMax), dim3(64), 0, s, a);
-        hipLaunchKernelGGL((k_hot_fill<Codec, Res, false>), gp, dim3(256), 0, s, a);
-    }
+    if (a.tok) hipLaunchKernelGGL((k_hot_fill<Codec, Res, true>), gp, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_hot_fill<Codec, Res, false>), gp, dim3(256), 0, s, a);
 }
 
-hipError_t launch_hot_chain(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
-    if (wide) hot_chain_launch<CodecW, uint64_t>(a, s);
-    else if (res_bytes == 1) hot_chain_launch<CodecC, uint8_t>(a, s);
-    else if (res_bytes == 2) hot_chain_launch<CodecC, uint16_t>(a, s);
-    else hot_chain_launch<CodecC, uint32_t>(a, s);
+hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
+    if (wide) hot_fill_launch<CodecW, uint64_t>(a, s);
+    else if (res_bytes == 1) hot_fill_launch<CodecC, uint8_t>(a, s);
+    else if (res_bytes == 2) hot_fill_launch<CodecC, uint16_t>(a, s);
+    else hot_fill_launch<CodecC, uint32_t>(a, s);
     return hipGetLastError();
 }
 

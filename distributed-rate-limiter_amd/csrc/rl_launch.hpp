@@ -87,14 +87,16 @@ struct RegionArgs {
     const uint32_t* hot_mark;  // [bins] nullable
     uint32_t epoch;
     HotInfo* hot_info;         // [kHotMax]
-    uint64_t* hot_summ;        // [chunks][4]: k_hot_summ's summary, then k_hot_chain's verdict
-    uint32_t* hot_total;       // total chunks over the listed regions
-    uint64_t* dbg;             // nullable (rl_tune "debug_regions"): per bin {t_start, t_end,
-                               // records, rounds}, t in s_memrealtime ticks (100 MHz)
+    uint64_t* hot_summ;        // [chunks][4]: k_hot_summ's summary, then the chain's verdict
+    uint64_t* hot_summ2;       // [groups][4]: the same over 64 chunks (4096 records)
+    uint32_t* hot_total;       // [0] chunks, [1] groups over the listed regions
+    uint64_t* dbg;             // nullable (rl_tune "debug_regions"): per bin kDbgWords words
+                               // {t_start, t_end, records, rounds, 4 x cycle counters}
 };
 
 constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
+constexpr uint32_t kDbgWords = 8;        // debug words per bin
 
 struct HotInfo {             // one listed hot region
     uint64_t tag;            // its dominant key (mix64 of the key hash)
@@ -103,6 +105,9 @@ struct HotInfo {             // one listed hot region
     uint32_t n_chunks;       // ceil((end - start) / kHotChunk)
     uint32_t chunk_base;     // index of its first chunk summary
     uint32_t ok;             // dominant key seen at least twice in the sample
+    uint32_t n_groups;       // ceil(n_chunks / 64)
+    uint32_t group_base;     // index of its first group summary
+    uint32_t pad[2];
 };
 
 struct BoundsArgs {
@@ -158,7 +163,7 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
                            uint32_t cols, hipStream_t s);
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s);   // prep, scan, summaries
-hipError_t launch_hot_chain(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);  // chain, fill
+hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
 hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
                              uint32_t n_bins, uint32_t threshold, uint32_t* hot_list,
                              uint32_t* hot_count, uint32_t* hot_mark, uint32_t epoch,

@@ -178,8 +178,8 @@ int  rl_sync(rl_engine* e);
  * measurement-only kernel variants whose results are NOT valid (0 = product path). */
 int  rl_tune(rl_engine* e, const char* key, int64_t value);
 /* Diagnostics (not needed by callers). "region_times": after a batch run with
- * rl_tune("debug_regions", 1), copies per-bin {t_start, t_end, records, rounds}
- * (uint64 x4; s_memrealtime ticks; rounds bit 63 = handled by the hot-region kernel).
+ * rl_tune("debug_regions", 1), copies per-bin {t_start, t_end, records, rounds,
+ * 4 cycle counters} (uint64 x8; s_memrealtime ticks; rounds bit 63 = a hot region).
  * Returns the number of bins copied (>= 0) or a status < 0. */
 int  rl_debug_fetch(rl_engine* e, const char* what, void* out, size_t bytes);
 const char* rl_strerror(int status);

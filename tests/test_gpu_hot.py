@@ -138,4 +138,4 @@ def test_hot_stats_and_device_entry():
     s = e.stats()
     assert s["allowed"] == int(want[0].sum())
     assert s["distinct_keys"] == len(np.unique(tr[0]))
-    assert e.stage_times()["region_hot"] > 0
+    assert e.stage_times()["hot_fill"] > 0

@@ -300,3 +300,18 @@ def test_zipf_trace_is_skewed():
     _, c = np.unique(keys.cpu().numpy(), return_counts=True)
     top = c.max() / n
     assert 0.09 < top < 0.13, top          # SURVEY: top key ~11.1% at s=1.1 over 100M keys
+
+
+@pytest.mark.parametrize("maxp,window", [(40, 1000), (1000, 60000), (3, 200)])
+def test_sw_same_key_runs_in_groups(maxp, window):
+    # few keys, dense arrivals: groups of 64 hold long same-key runs that mix allows,
+    # denials and window roll-overs (exercises both round hypotheses of wave_apply)
+    lims = [[rl_amd.SW, maxp, window, 0.0]]
+    rng = np.random.default_rng(maxp)
+    n = 400_000
+    keys = rl_amd.mix64(rng.integers(0, 40, n).astype(np.uint64) + np.uint64(99))
+    now = (T0 * NS + np.sort(rng.integers(0, 30 * window * NS, n))).astype(np.int64)
+    permits = rng.integers(1, 4, n).astype(np.int32)
+    op = np.where(rng.random(n) < 0.01, 1, 0).astype(np.uint8)
+    got, want, _ = run_both(lims, (keys, permits, now, np.zeros(n, np.uint16), op), batches=3)
+    assert_same(got, want, "sw runs")

@@ -51,12 +51,15 @@ for b in range(args.batches):
     dur = (d[:, 1] - d[:, 0]) / 100.0          # us
     hot = (d[:, 3] >> np.uint64(63)) == 1
     rounds = d[:, 3] & np.uint64((1 << 63) - 1)
-    print(f"batch {b}: region stage {st['region']:.2f} ms hot {st['region_hot']:.2f} ms; "
+    print(f"batch {b}: region stage {st['region']:.2f} ms hot {st['hot_fill']:.2f} ms; "
           f"{len(d)} regions, {hot.sum()} hot; span {(d[:, 1].max() - t0) / 100:.0f} us")
     order = np.argsort(-dur)[:12]
     for i in order:
-        print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  recs {int(d[i, 2]):9d} "
-              f"rounds {int(rounds[i]):8d} {'HOT' if hot[i] else ''}")
+        rr = int(rounds[i])
+        cyc = " ".join(f"{x / 1e6:6.2f}" for x in d[i, 4:8])
+        what = (f"detail {rr & 0xFFFFFFFF:7d} (other keys {rr >> 32:7d}) HOT Mcyc det/run/srch/p2 {cyc}"
+                if hot[i] else f"rounds {rr:8d}")
+        print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  recs {int(d[i, 2]):9d} {what}")
     nh = ~hot
     ends = (d[nh, 1] - t0) / 100
     for q in (0.5, 0.9, 0.99, 0.999, 1.0):
