@@ -48,6 +48,32 @@ CONFIGS = {
                     dist=rl_amd.DIST_ZIPF, zipf_s=1.1, batch=1 << 28, span_ns=60_000 * NS,
                     permits_max=1, seed=0x5EED0003, capacity=30_000_000,
                     desc="SW 1000/min window 60s; 100M keys Zipf s=1.1; 256M requests over 60 s"),
+    # configs[3]: 10 limiter configs (RateLimiterConfig.java:51-92 + RateLimitConfig.java:61-80
+    # factories + TB variants), each key owned by one limiter (rank % 10), Zipf s=1.1; the
+    # config is 500M keys on 4 GPUs: 125M keys and 128M requests per GPU per step
+    "mixed_tenants": dict(limiters=[(rl_amd.SW, 10, 60_000, 0.0),        # login / authRateLimiter
+                                    (rl_amd.SW, 100, 60_000, 0.0),       # api (cache off)
+                                    (rl_amd.TB, 50, 60_000, 10.0),       # burst
+                                    (rl_amd.SW, 5, 1_000, 0.0),          # perSecond(5)
+                                    (rl_amd.SW, 100, 1_000, 0.0),        # perSecond(100)
+                                    (rl_amd.SW, 1000, 60_000, 0.0),      # perMinute(1000)
+                                    (rl_amd.SW, 5000, 3_600_000, 0.0),   # perHour(5000)
+                                    (rl_amd.TB, 10, 10_000, 1.0),
+                                    (rl_amd.TB, 1000, 60_000, 100.0),
+                                    (rl_amd.TB, 100, 300_000, 0.5)],
+                          n_keys=125_000_000, dist=rl_amd.DIST_ZIPF, zipf_s=1.1, batch=1 << 27,
+                          span_ns=60_000 * NS, permits_max=2, seed=0x5EED0004,
+                          capacity=16_000_000,
+                          desc="10 limiters (login 10/min, api 100/min, burst TB 50@10/s, 7 "
+                               "variants); Zipf s=1.1; 125M keys + 128M requests per GPU per "
+                               "step over 60 s (500M keys at 4 GPUs)"),
+    # configs[4]: 1B keys over 8 GPUs, TB(50, 10/s) + SW(1000/min) by key rank, Zipf s=1.1,
+    # 2^30 requests per step: 125M keys and 2^27 requests per GPU
+    "zipf_1b": dict(limiters=[(rl_amd.TB, 50, 60_000, 10.0), (rl_amd.SW, 1000, 60_000, 0.0)],
+                    n_keys=125_000_000, dist=rl_amd.DIST_ZIPF, zipf_s=1.1, batch=1 << 27,
+                    span_ns=60_000 * NS, permits_max=1, seed=0x5EED0005, capacity=24_000_000,
+                    desc="TB 50@10/s + SW 1000/min; Zipf s=1.1; 125M keys + 2^27 requests per "
+                         "GPU per step over 60 s (1B keys, 2^30 requests at 8 GPUs)"),
 }
 
 # algorithmic bytes per request / per distinct key
@@ -146,17 +172,19 @@ def main():
 
     dev = torch.device("cuda", local)
     n_global_total = total_steps * ws * n
+    n_lim = len(cfg["limiters"])
     inputs = []
     for s in range(total_steps):
         keys = torch.empty(n, dtype=torch.int64, device=dev)
         permits = torch.empty(n, dtype=torch.int32, device=dev)
         now = torch.empty(n, dtype=torch.int64, device=dev)
-        eng.synth_trace(n, keys, permits, now, None, seed=cfg["seed"], n_keys=cfg["n_keys"] * ws,
+        lim = torch.empty(n, dtype=torch.int16, device=dev) if n_lim > 1 else None
+        eng.synth_trace(n, keys, permits, now, lim, seed=cfg["seed"], n_keys=cfg["n_keys"] * ws,
                         dist=cfg["dist"], zipf_s=cfg.get("zipf_s", 1.1),
                         permits_max=cfg["permits_max"], t0_ns=T0_NS,
                         span_ns=cfg["span_ns"] * total_steps,
-                        index_base=(s * ws + rank) * n, n_total=n_global_total, n_limiters=1)
-        inputs.append((keys, permits, now))
+                        index_base=(s * ws + rank) * n, n_total=n_global_total, n_limiters=n_lim)
+        inputs.append((keys, permits, now, lim))
     allowed = torch.empty(n, dtype=torch.uint8, device=dev)
     remaining = torch.empty(n, dtype=torch.int64, device=dev)
     eng.sync()
@@ -167,11 +195,12 @@ def main():
         router = Router(DeviceOps(eng, ws, dev, n), ws, rank)
 
         def step(s):
-            router.step(*inputs[s], allowed, remaining)
+            k, p, t, li = inputs[s]
+            router.step(k, p, t, allowed, remaining, li)
     else:
         def step(s):
-            k, p, t = inputs[s]
-            eng.execute_device(n, k, p, t, None, None, allowed, remaining)
+            k, p, t, li = inputs[s]
+            eng.execute_device(n, k, p, t, li, None, allowed, remaining)
 
     keep0 = None
     for s in range(warm):
@@ -222,10 +251,10 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64" if cfg["limiters"][0][0] == rl_amd.TB else "int64+f64",
+        "dtype": "f64" if all(l[0] == rl_amd.TB for l in cfg["limiters"]) else "int64+f64",
         "data": "synthetic (deterministic splitmix64 trace generated on device)",
         "config": {"workload": f"{args.config}: {cfg['desc']}", "requests_per_gpu_per_step": n,
-                   "n_keys": cfg["n_keys"] * ws, "parallelism": f"key-hash shards x{ws}"
+                   "n_keys": cfg["n_keys"] * ws, "n_limiters": n_lim, "parallelism": f"key-hash shards x{ws}"
                    + (" + RCCL all-to-all routing" if ws > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom,
@@ -238,8 +267,8 @@ def main():
         "status": rl_amd.strerror(st),
     }
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        k0, p0, t0_ = inputs[0]
-        cb, parity, m = cpu_baseline(cfg, k0, p0, t0_, None, args.cpu_sample, keep0[0], keep0[1])
+        k0, p0, t0_, l0 = inputs[0]
+        cb, parity, m = cpu_baseline(cfg, k0, p0, t0_, l0, args.cpu_sample, keep0[0], keep0[1])
         out["cpu_baseline"] = cb
         out["parity"] = f"{'bit-exact' if parity else 'MISMATCH'} vs oracle on the first {m} " \
                         f"requests of batch 0"

@@ -53,7 +53,7 @@ constexpr uint32_t kPermitMask = (1u << kPermitBits) - 1;   // 0 = invalid marke
 constexpr int64_t kCompactMaxPermits = (int64_t)kPermitMask - 1;  // clamp is exact below this
 
 // ---------------------------------------------------------------- limiter table
-struct DevLimiter {          // 64 B, read-only during a batch
+struct DevLimiter {          // 80 B, read-only during a batch
     int32_t algo;
     int32_t region_bits;     // k: the limiter has 2^k regions
     uint32_t region_base;    // first global region id
@@ -64,6 +64,8 @@ struct DevLimiter {          // 64 B, read-only during a batch
     double rate_per_ms;      // TB: refillRate / 1000.0 (TokenBucketRateLimiter.java:85)
     double capacity;         // TB: (double)maxPermits (Lua tonumber(ARGV[1]))
     uint64_t table;          // device address of this limiter's region array
+    double inv_window;       // 1.0 / w: first guess of Java's now / w (jdiv corrects it)
+    uint64_t pad1;
 };
 
 // One 32-byte slot of a region (HBM and the LDS image).
@@ -278,8 +280,8 @@ __device__ inline int64_t sw_get(const SW2& s, int64_t start, int64_t now, int64
 
 // Java long division / remainder (truncating) by 0 < w < 2^31, exact for |a| < 2^53:
 // a correctly rounded fp64 quotient is within 1 of the true one; fix it up in integers.
-__device__ inline int64_t jdiv(int64_t a, int64_t w, int64_t* rem) {
-    int64_t q = (int64_t)((double)a / (double)w);
+__device__ inline int64_t jdiv(int64_t a, int64_t w, double inv_w, int64_t* rem) {
+    int64_t q = (int64_t)((double)a * inv_w);              // within 1 of the quotient
     int64_t r = a - q * w;
     if (r < 0 && a >= 0) { q -= 1; r += w; }
     else if (r >= w) { q += 1; r -= w; }
@@ -295,12 +297,16 @@ struct SWGeo {
     double prev_weight;      // 1.0 - (double)(now % w) / w   (:170-171)
 };
 
-__device__ inline SWGeo sw_geo(int64_t now, int64_t w) {
+// One true division (the IEEE quotient Java computes, :170); the window starts come from
+// a reciprocal multiply corrected in integers.
+__device__ inline SWGeo sw_geo(int64_t now, const DevLimiter& L) {
+    const int64_t w = L.window_ms;
     SWGeo g;
     int64_t r, r2;
-    const int64_t q = jdiv(now, w, &r);
+    const int64_t q = jdiv(now, w, L.inv_window, &r);
     g.curr_start = q * w;
-    g.prev_start = jdiv(now - w, w, &r2) * w;
+    // (now - w) / w == now / w - 1 under truncation iff now >= w (near the epoch it differs)
+    g.prev_start = now >= w ? g.curr_start - w : jdiv(now - w, w, L.inv_window, &r2) * w;
     const double pct = (double)r / (double)w;
     g.prev_weight = 1.0 - pct;
     return g;
@@ -364,7 +370,7 @@ __device__ inline Outcome sw_step_g(const DevLimiter& L, uint32_t op, int32_t pe
 
 __device__ inline Outcome sw_step(const DevLimiter& L, uint32_t op, int32_t permits,
                                   int64_t now, uint64_t a, uint64_t b, uint64_t c) {
-    return sw_step_g(L, op, permits, now, sw_geo(now, L.window_ms), a, b, c);
+    return sw_step_g(L, op, permits, now, sw_geo(now, L), a, b, c);
 }
 
 // Sliding-window acquire at `now` assuming that k earlier requests of the same key, all

@@ -457,7 +457,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
     SWGeo geo{};
     uint64_t same_w = 0, elig_m = 0;        // (A): lanes in my window / acquires
     if constexpr (!tb) {
-        if (slot >= 0) geo = sw_geo(q.now_ms, L.window_ms);
+        if (slot >= 0) geo = sw_geo(q.now_ms, L);
         // window index relative to the wave's first window (2 bits; 3 = "far")
         int64_t wmin = slot >= 0 ? geo.curr_start : INT64_MAX;
         for (int o = 32; o > 0; o >>= 1) {
@@ -719,7 +719,7 @@ __device__ inline bool hot_pred(const DevLimiter& L, int64_t t, uint64_t a, uint
         return tb_refill(L, t, a, b, c) >= 1.0;
     } else {
         const SW2 s = sw_unpack(a, b, c);
-        return sw_estimate(s, sw_geo(t, L.window_ms), t, L.window_ms) < L.max_permits;
+        return sw_estimate(s, sw_geo(t, L), t, L.window_ms) < L.max_permits;
     }
 }
 
@@ -766,13 +766,62 @@ __device__ inline int64_t wave_first_true(int64_t s, int64_t hi, uint32_t lane, 
     return lo;
 }
 
+// Approximate first t >= s with hot_pred(t) from the closed forms (only a starting
+// point: hot_thresholds checks it exactly). Returns s when there is no useful estimate.
+template <int ALGO>
+__device__ inline int64_t hot_t1_guess(const DevLimiter& L, int64_t s, uint64_t a, uint64_t b,
+                                       uint64_t c) {
+    if constexpr (ALGO == kAlgoTB) {
+        if (!(c & 1u)) return s;                                // absent: full at every t
+        const double tok0 = __longlong_as_double((long long)a);
+        const int64_t last = (int64_t)b;
+        if (!(tok0 < 1.0) || !(L.rate_per_ms > 0.0)) return s;
+        const double te = (double)last + ceil((1.0 - tok0) / L.rate_per_ms);
+        int64_t g = te < 4.0e18 ? (int64_t)te : INT64_MAX / 4;
+        const int64_t full = last + L.ttl_ms + 1;               // expired: full again
+        return g < full ? g : full;
+    } else {
+        const int64_t w = L.window_ms;
+        const SW2 st = sw_unpack(a, b, c);
+        const SWGeo g0 = sw_geo(s, L);
+        const int64_t C = sw_get(st, g0.curr_start, s, w);
+        const int64_t P = sw_get(st, g0.prev_start, s, w);
+        if (C >= L.max_permits || P == 0) return s;
+        const double rr = (double)w * (1.0 - (double)(L.max_permits - C) / (double)P);
+        int64_t g = g0.curr_start + (int64_t)floor(rr) + 1;
+        int64_t lastp = INT64_MAX / 4;                          // previous bucket's TTL lapse
+        if (st.b1_start == g0.prev_start) lastp = st.b1_start + st.b1_off;
+        else if (st.b1_start == g0.curr_start) lastp = g0.prev_start + st.b0_off;
+        if (g > lastp + w + 1) g = lastp + w + 1;
+        const int64_t wend = g0.curr_start + w;                 // next window: a new geometry
+        return g < wend ? g : wend;
+    }
+}
+
 template <int ALGO>
 __device__ inline void hot_thresholds(const DevLimiter& L, uint64_t a, uint64_t b, uint64_t c,
                                       int64_t from, int64_t lo, int64_t hi, uint32_t lane,
                                       int64_t* T0, int64_t* T1) {
     const int64_t t0 = hot_t0<ALGO>(lo, hi, a, b, c);
     const int64_t s = from > t0 ? from : t0;
-    int64_t t1 = wave_first_true(s, hi, lane, [&](int64_t t) { return hot_pred<ALGO>(L, t, a, b, c); });
+    auto pred = [&](int64_t t) { return hot_pred<ALGO>(L, t, a, b, c); };
+    int64_t t1 = hi + 1;
+    bool found = false;
+    // First an estimate from the closed form of the refill / the window weight, checked
+    // exactly at the 64 times around it (one ballot: the predicate is monotone, so a
+    // false -> true step inside the probed times is the answer); the full search only if
+    // the step lies outside them.
+    int64_t g = hot_t1_guess<ALGO>(L, s, a, b, c);
+    if (g > s + 32) {
+        int64_t t = g - 32 + (int64_t)lane;
+        if (t > hi) t = hi;
+        const uint64_t m = __ballot(pred(t));
+        if (m != 0 && !(m & 1u)) {
+            t1 = __shfl(t, (int)__builtin_ctzll(m), 64);
+            found = true;
+        }
+    }
+    if (!found) t1 = wave_first_true(s, hi, lane, pred);
     if (t1 == s) t1 = t0;        // pred(s) already true: [t0, s) undecided -> empty range
     *T0 = t0;
     *T1 = t1;
@@ -1031,6 +1080,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         // then the request that finds the key at its limit again).
         Rec pre = recs[min(f.start + lane, f.end - 1)];
         uint32_t pre_c = 0;
+        uint32_t prev_detail = 0xFFFFFFF0u;               // last chunk processed here
+        bool stale = false;                               // [T0, T1) emptied, not searched
         auto detail = [&](uint32_t c) {
             ++n_detail;
             const uint64_t c_det = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
@@ -1048,7 +1099,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 out = pack_result(false, kRemUnknown);    // :110-116, no state access
                 pend = false;
             }
-            for (;;) {
+            {
                 const bool fast = q.op == (uint32_t)kOpAcquire && q.now_ms >= T0 && q.now_ms < T1;
                 const uint64_t m = __ballot(pend && !fast);
                 const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
@@ -1057,37 +1108,102 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                     if (TOK && A == kAlgoTB) tk = tb_refill(L, q.now_ms, S.sa[hs], S.sb[hs], S.sc[hs]);
                     pend = false;
                 }
-                if (first == 64u) break;
-                // sequential run from `first`, state in registers, until a (deny, 0)
+            }
+            if (__any(pend)) {
+                // The rest of the key's requests in this chunk, in rounds (as wave_apply,
+                // all lanes are one key): (D) the prefix up to the first state change, or
+                // (A, sliding window) up to the first denial assuming every earlier pending
+                // request allowed, whichever is longer. State in registers.
                 const uint64_t c_run = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-                const uint64_t pm = __ballot(pend);
+                SWGeo geo{};
+                uint64_t same_w = 0, elig_m = 0;
+                if constexpr (A != kAlgoTB) {
+                    if (pend) geo = sw_geo(q.now_ms, L);
+                    int64_t wmin = pend ? geo.curr_start : INT64_MAX;
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const int64_t x = __shfl_xor(wmin, o, 64);
+                        wmin = x < wmin ? x : wmin;
+                    }
+                    const bool w0 = pend && geo.curr_start == wmin;
+                    same_w = __ballot(w0);
+                    elig_m = __ballot(w0 && q.op == (uint32_t)kOpAcquire);
+                }
                 uint64_t sa = S.sa[hs], sb = S.sb[hs], sc = S.sc[hs];
-                uint32_t flag = 0;
-                int64_t from = 0;
-                for (uint32_t jj = first; jj < 64; ++jj) {
-                    if (!((pm >> jj) & 1u)) continue;
-                    const int64_t now = __shfl(q.now_ms, (int)jj, 64);
-                    const int32_t pj = __shfl(q.permits, (int)jj, 64);
-                    const uint32_t op = (uint32_t)__shfl((int)q.op, (int)jj, 64);
-                    Outcome o;
-                    if constexpr (A == kAlgoTB) o = tb_step(L, op, pj, now, sa, sb, sc);
-                    else o = sw_step(L, op, pj, now, sa, sb, sc);
-                    if (o.mutate) { sa = o.a; sb = o.b; sc = o.c; flag |= 1u; from = now; }
-                    if (lane == jj) { out = pack_result(o.allowed, o.remaining); tk = o.tokens; pend = false; }
-                    if (lane == 0 && o.allowed) ++n_allowed;
-                    if (!o.mutate && !o.allowed && o.remaining == 0 && op == (uint32_t)kOpAcquire) {
-                        flag |= 2u;
-                        from = now;
-                        break;
+                bool changed = false;
+                while (__any(pend)) {
+                    const uint64_t pm = __ballot(pend);
+                    Outcome o{};
+                    SWAllow al{false, 0};
+                    bool elig = false;
+                    if (pend) {
+                        if constexpr (A == kAlgoTB) {
+                            o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
+                        } else {
+                            o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc);
+                            elig = (pm & ~(elig_m & same_w)) == 0 && (pm & (pm - 1)) != 0 &&
+                                   (int64_t)sa <= geo.curr_start;
+                            if (elig) al = sw_try_after_allows(L, q.permits, q.now_ms, geo, sa, sb, sc,
+                                                               popc_below(pm));
+                        }
+                    }
+                    const uint64_t mut = __ballot(pend && o.mutate);
+                    const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
+                    uint32_t fa = 0;
+                    bool use_a = false;
+                    if constexpr (A != kAlgoTB) {
+                        const uint64_t den = __ballot(pend && elig && !al.allowed);
+                        fa = den ? (uint32_t)__builtin_ctzll(den) : 64u;
+                        use_a = __any(elig) && fa > fm;
+                    }
+                    if (use_a) {
+                        if constexpr (A != kAlgoTB) {
+                            const uint64_t ok = pm & (fa >= 64u ? ~0ULL : ((1ULL << fa) - 1));
+                            const uint32_t last = 63u - (uint32_t)__builtin_clzll(ok);
+                            const int64_t t_last = __shfl(q.now_ms, (int)last, 64);
+                            SWGeo gl;                     // every lane commits the same state
+                            gl.curr_start = __shfl(geo.curr_start, (int)last, 64);
+                            gl.prev_start = __shfl(geo.prev_start, (int)last, 64);
+                            gl.prev_weight = __shfl(geo.prev_weight, (int)last, 64);
+                            sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)__popcll(ok), t_last);
+                            if (pend && lane <= fa) {
+                                out = pack_result(al.allowed, al.remaining);
+                                n_allowed += al.allowed ? 1u : 0u;
+                                pend = false;
+                            }
+                            changed = true;
+                        }
+                    } else {
+                        if (pend && lane <= fm) {
+                            out = pack_result(o.allowed, o.remaining);
+                            tk = o.tokens;
+                            n_allowed += o.allowed ? 1u : 0u;
+                            pend = false;
+                        }
+                        if (fm < 64u) {
+                            sa = __shfl(o.a, (int)fm, 64);
+                            sb = __shfl(o.b, (int)fm, 64);
+                            sc = __shfl(o.c, (int)fm, 64);
+                            changed = true;
+                        }
                     }
                 }
                 wave_fence();
                 if (lane == 0) { S.sa[hs] = sa; S.sb[hs] = sb; S.sc[hs] = sc; }
                 wave_fence();
-                // (deny, 0) at `from`, or the run ended after a state change at `from`:
-                // search T1 from there (an empty range if the key is below its limit)
+                // thresholds for the next chunks: search from this chunk's last hot request,
+                // unless the key changes state chunk after chunk (then no chunk could be
+                // skipped anyway: leave the range empty until a chunk without a change)
                 const uint64_t c_srch = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-                if (flag) hot_thresholds<A>(L, sa, sb, sc, from, lo, hi, lane, &T0, &T1);
+                const bool dense = c == prev_detail + 1;
+                if (changed && dense) {
+                    T1 = T0;
+                    stale = true;
+                } else if (changed || stale) {
+                    const uint64_t hm = __ballot(hot);
+                    const int64_t from = __shfl(q.now_ms, 63 - __builtin_clzll(hm), 64);
+                    hot_thresholds<A>(L, sa, sb, sc, from, lo, hi, lane, &T0, &T1);
+                    stale = false;
+                }
                 if (a.dbg) {
                     const uint64_t c_end = __builtin_amdgcn_s_memtime();
                     cyc_run += c_srch - c_run;
@@ -1098,6 +1214,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 res[j] = (Res)out;
                 if (TOK) a.tok[j] = tk;
             }
+            prev_detail = c;
             if (a.dbg) cyc_detail += __builtin_amdgcn_s_memtime() - c_det;
         };
         // level 1: the chunks of one group of 64

@@ -24,7 +24,8 @@ def _trace(steps, world, n):
     keys = rl_amd.mix64(ranks.astype(np.uint64))
     permits = rng.integers(1, 5, total).astype(np.int32)
     now = (T0 * NS + np.sort(rng.integers(0, 30_000 * NS, total))).astype(np.int64)
-    return keys, permits, now
+    lim = (ranks % 2).astype(np.uint16)                  # each key belongs to one limiter
+    return keys, permits, now, lim
 
 
 def _worker(rank, world, port, steps, n, out):
@@ -37,17 +38,19 @@ def _worker(rank, world, port, steps, n, out):
     eng = rl_amd.Engine(device=0, max_batch=4 * n, capacity=1 << 16, shard_index=rank,
                         shard_count=world)
     eng.add_limiter(rl_amd.TB, 50, 60000, 10.0)
+    eng.add_limiter(rl_amd.SW, 30, 5000, 0.0)
     router = Router(DeviceOps(eng, world, dev, n), world, rank, exchange_device="cpu")
-    keys, permits, now = _trace(steps, world, n)
+    keys, permits, now, lim = _trace(steps, world, n)
     res_a, res_r = [], []
     for s in range(steps):
         sl = slice((s * world + rank) * n, (s * world + rank + 1) * n)
         k = torch.from_numpy(keys[sl].view(np.int64).copy()).to(dev)
         p = torch.from_numpy(permits[sl].copy()).to(dev)
         t = torch.from_numpy(now[sl].copy()).to(dev)
+        li = torch.from_numpy(lim[sl].view(np.int16).copy()).to(dev)
         a = torch.empty(n, dtype=torch.uint8, device=dev)
         r = torch.empty(n, dtype=torch.int64, device=dev)
-        router.step(k, p, t, a, r)
+        router.step(k, p, t, a, r, li)
         eng.sync()
         res_a.append(a.cpu().numpy())
         res_r.append(r.cpu().numpy())
@@ -65,8 +68,9 @@ def test_two_shards_one_gpu(tmp_path):
     world, steps, n = 2, 3, 100_000
     out = str(tmp_path / "r")
     mp.spawn(_worker, args=(world, port, steps, n, out), nprocs=world, join=True)
-    keys, permits, now = _trace(steps, world, n)
-    wa, wr, _, _ = COracle([[1, 50, 60000, 10.0]]).run(keys, permits, now, want_tokens=False)
+    keys, permits, now, lim = _trace(steps, world, n)
+    wa, wr, _, _ = COracle([[1, 50, 60000, 10.0], [0, 30, 5000, 0.0]]).run(
+        keys, permits, now, lim, want_tokens=False)
     for rank in range(world):
         d = np.load(f"{out}.{rank}.npz")
         for st in range(steps):

@@ -30,18 +30,19 @@ class HostOps:
         self.perm = np.argsort(own, kind="stable")
         return np.bincount(own, minlength=self.world).tolist()
 
-    def pack(self, n, keys, permits, now):
-        self.lim = None
-        return (keys[self.perm].clone(), permits[self.perm].clone(), now[self.perm].clone())
+    def pack(self, n, keys, permits, now, limiter=None):
+        return (keys[self.perm].clone(), permits[self.perm].clone(), now[self.perm].clone(),
+                None if limiter is None else limiter[self.perm].clone())
 
-    def recv_buffers(self, m):
+    def recv_buffers(self, m, with_limiter=False):
         return (torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32),
-                torch.empty(m, dtype=torch.int64))
+                torch.empty(m, dtype=torch.int64),
+                torch.empty(m, dtype=torch.int16) if with_limiter else None)
 
-    def decide(self, m, k, p, t):
+    def decide(self, m, k, p, t, lim=None):
         kk = k.numpy().view(np.uint64)
-        lim = (kk % np.uint64(2)).astype(np.uint16)      # limiter derived from the key
-        a, r, _, _ = self.o.run(kk, p.numpy(), t.numpy(), lim, None, want_tokens=False)
+        lm = None if lim is None else lim.numpy().view(np.uint16)
+        a, r, _, _ = self.o.run(kk, p.numpy(), t.numpy(), lm, None, want_tokens=False)
         return torch.from_numpy(r * 2 + a.astype(np.int64))
 
     def back_buffer(self, n):
@@ -63,13 +64,14 @@ def global_trace(steps, world, n):
     keys = rl_amd.mix64(ranks.astype(np.uint64))
     permits = rng.integers(1, 5, total).astype(np.int32)
     now = (T0 * NS + np.sort(rng.integers(0, 20_000 * NS, total))).astype(np.int64)
-    return keys, permits, now
+    lim = (ranks % len(LIMS)).astype(np.uint16)          # each key belongs to one limiter
+    return keys, permits, now, lim
 
 
 def _worker(rank, world, port, steps, n, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    keys, permits, now = global_trace(steps, world, n)
+    keys, permits, now, lim = global_trace(steps, world, n)
     router = Router(HostOps(world), world, rank)
     got_a, got_r = [], []
     for s in range(steps):
@@ -77,9 +79,10 @@ def _worker(rank, world, port, steps, n, out_path):
         k = torch.from_numpy(keys[sl].view(np.int64).copy())
         p = torch.from_numpy(permits[sl].copy())
         t = torch.from_numpy(now[sl].copy())
+        li = torch.from_numpy(lim[sl].view(np.int16).copy())
         a = torch.empty(n, dtype=torch.uint8)
         r = torch.empty(n, dtype=torch.int64)
-        router.step(k, p, t, a, r)
+        router.step(k, p, t, a, r, li)
         got_a.append(a.numpy().copy())
         got_r.append(r.numpy().copy())
     np.savez(f"{out_path}.{rank}.npz", a=np.concatenate(got_a), r=np.concatenate(got_r))
@@ -99,8 +102,7 @@ def test_router_matches_single_process_oracle(tmp_path, world):
     steps, n = 3, 3000
     out = str(tmp_path / "res")
     mp.spawn(_worker, args=(world, _free_port(), steps, n, out), nprocs=world, join=True)
-    keys, permits, now = global_trace(steps, world, n)
-    lim = (keys % np.uint64(2)).astype(np.uint16)
+    keys, permits, now, lim = global_trace(steps, world, n)
     wa, wr, _, _ = COracle(LIMS).run(keys, permits, now, lim, None, want_tokens=False)
     for rank in range(world):
         d = np.load(f"{out}.{rank}.npz")

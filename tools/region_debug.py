@@ -35,14 +35,15 @@ permits = torch.empty(n, dtype=torch.int32, device=dev)
 now = torch.empty(n, dtype=torch.int64, device=dev)
 allowed = torch.empty(n, dtype=torch.uint8, device=dev)
 remaining = torch.empty(n, dtype=torch.int64, device=dev)
-import ctypes  # noqa: E402
+n_lim = len(cfg["limiters"])
+lim = torch.empty(n, dtype=torch.int16, device=dev) if n_lim > 1 else None
 nb = 1 << 24
 for b in range(args.batches):
-    eng.synth_trace(n, keys, permits, now, None, seed=cfg["seed"], n_keys=cfg["n_keys"],
+    eng.synth_trace(n, keys, permits, now, lim, seed=cfg["seed"], n_keys=cfg["n_keys"],
                     dist=cfg["dist"], zipf_s=cfg.get("zipf_s", 1.1), permits_max=cfg["permits_max"],
                     t0_ns=T0_NS, span_ns=cfg["span_ns"] * args.batches, index_base=b * n,
-                    n_total=n * args.batches)
-    eng.execute_device(n, keys, permits, now, None, None, allowed, remaining)
+                    n_total=n * args.batches, n_limiters=n_lim)
+    eng.execute_device(n, keys, permits, now, lim, None, allowed, remaining)
     eng.sync()
     st = eng.stage_times()
     d = eng.debug_region_times(nb)
