@@ -513,6 +513,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     mark(e, 8);
     UnpermArgs ua{};
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
+    ua.mid = e->rec0;                                    // pass-0 records are dead by now
     ua.tok = tokens_after ? e->tok : nullptr;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
     ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate; ua.per_cu = e->un_per_cu;

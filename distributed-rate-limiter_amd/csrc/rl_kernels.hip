@@ -1611,6 +1611,35 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
   }
 }
 
+// Two-pass batches: undo the high-digit pass first. mid[j] = res[pos1[j]] for j in
+// pass-0 order: pos1 is read in order and, since pass 0 left the records sorted by low
+// digit, consecutive j fall into one low-digit run whose elements go to the 2^d1
+// high-digit bins in order — the gather walks 2^d1 sequential streams instead of the
+// whole result array. k_unpermute then gathers mid[pos0[i]] (2^d0 streams). Two
+// local gathers replace the composed res[pos1[pos0[i]]], which hit a random line of a
+// 1 GB index and of the result array per request.
+template <class Res>
+__global__ __launch_bounds__(256) void k_unpermute_mid(const uint32_t* __restrict__ pos1,
+                                                       const Res* __restrict__ res,
+                                                       Res* __restrict__ mid, uint32_t n) {
+    constexpr int B = 8;
+    const uint32_t base = blockIdx.x * (256u * B) + threadIdx.x;
+    uint32_t p[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const uint32_t j = base + (uint32_t)k * 256u;
+        p[k] = pos1[j < n ? j : 0];
+    }
+    Res v[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const uint32_t j = base + (uint32_t)k * 256u;
+        if (j < n) mid[j] = v[k];
+    }
+}
+
 __global__ void k_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
@@ -1892,7 +1921,22 @@ hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_unpermute(const UnpermArgs& a, int res_bytes, hipStream_t s) {
+template <class Res>
+static void unpermute_mid(const UnpermArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_unpermute_mid<Res>, dim3((a.n + 2047) / 2048), dim3(256), 0, s, a.pos1,
+                       (const Res*)a.res, (Res*)a.mid, a.n);
+}
+
+hipError_t launch_unpermute(const UnpermArgs& a_in, int res_bytes, hipStream_t s) {
+    UnpermArgs a = a_in;
+    if (a.pos1 && a.mid && !a.tokens_out && a.n) {      // two-pass: undo pass 1, then pass 0
+        if (res_bytes == 8) unpermute_mid<uint64_t>(a, s);
+        else if (res_bytes == 1) unpermute_mid<uint8_t>(a, s);
+        else if (res_bytes == 2) unpermute_mid<uint16_t>(a, s);
+        else unpermute_mid<uint32_t>(a, s);
+        a.res = a.mid;
+        a.pos1 = nullptr;
+    }
     dim3 g(persistent_grid(a.n_tiles, a.per_cu ? a.per_cu : 1)), b(kTileThreads);
     if (res_bytes == 8) hipLaunchKernelGGL(k_unpermute<uint64_t>, g, b, 0, s, a);
     else if (res_bytes == 1) hipLaunchKernelGGL(k_unpermute<uint8_t>, g, b, 0, s, a);

@@ -126,6 +126,7 @@ struct UnpermArgs {
     const uint32_t* pos1;      // nullable
     const void* res;
     const double* tok;         // nullable
+    void* mid;                 // nullable: n results of scratch (two-pass batches)
     uint8_t* allowed;
     int64_t* remaining;
     double* tokens_out;        // nullable
