@@ -779,6 +779,72 @@ extern "C" int rl_route_unpack(rl_engine* e, size_t n, const uint32_t* perm, con
     return RL_OK;
 }
 
+extern "C" int rl_route_pack_wire(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key,
+                                  const int32_t* permits, const int64_t* now_ns,
+                                  const uint16_t* limiter, uint64_t* wire_out,
+                                  uint16_t* limiter_out, int64_t* hdr, void* stream) {
+    if (!e || !hdr || (n && (!perm || !key || !permits || !now_ns || !wire_out))) return RL_E_INVALID_ARG;
+    if (n > 0xFFFFFFF0ULL) return RL_E_TOO_LARGE;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_pack_wire((uint32_t)n, perm, key, permits, now_ns, limiter, wire_out,
+                                  limiter_out, hdr, s));
+    return RL_OK;
+}
+
+extern "C" int rl_route_unwire(rl_engine* e, size_t m, const uint64_t* wire, uint32_t n_src,
+                               const int64_t* src_base, const uint64_t* src_count,
+                               uint64_t* key_out, int32_t* permits_out, int64_t* now_out,
+                               void* stream) {
+    if (!e || !src_base || !src_count || n_src == 0 || n_src > (uint32_t)kMaxShards)
+        return RL_E_INVALID_ARG;
+    if (m && (!wire || !key_out || !permits_out || !now_out)) return RL_E_INVALID_ARG;
+    if (m > 0xFFFFFFF0ULL) return RL_E_TOO_LARGE;
+    uint32_t end[kMaxShards];
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < n_src; ++i) { run += src_count[i]; end[i] = (uint32_t)run; }
+    if (run != m) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_unwire((uint32_t)m, wire, n_src, src_base, end, key_out, permits_out,
+                               now_out, s));
+    return RL_OK;
+}
+
+extern "C" int rl_result_width(rl_engine* e) {
+    if (!e) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    bool wide = false;
+    int64_t max_any = 0;
+    for (auto& l : e->lims) {
+        wide |= l.cfg.max_permits > kCompactMaxPermits;
+        max_any = std::max<int64_t>(max_any, l.cfg.max_permits);
+    }
+    return res_bytes_for(max_any, wide);
+}
+
+extern "C" int rl_route_fold_packed(rl_engine* e, size_t n, const uint8_t* allowed,
+                                    const int64_t* remaining, void* packed, int width,
+                                    void* stream) {
+    if (!e || (n && (!allowed || !remaining || !packed))) return RL_E_INVALID_ARG;
+    if (width != 1 && width != 2 && width != 4 && width != 8) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_fold_w((uint32_t)n, allowed, remaining, packed, width, s));
+    return RL_OK;
+}
+
+extern "C" int rl_route_unpack_packed(rl_engine* e, size_t n, const uint32_t* perm,
+                                      const void* packed, int width, uint8_t* allowed,
+                                      int64_t* remaining, void* stream) {
+    if (!e || (n && (!perm || !packed || !allowed || !remaining))) return RL_E_INVALID_ARG;
+    if (width != 1 && width != 2 && width != 4 && width != 8) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_unpack_w((uint32_t)n, perm, packed, width, allowed, remaining, s));
+    return RL_OK;
+}
+
 extern "C" int rl_synth_trace_device(rl_engine* e, const rl_trace_spec* sp, size_t n,
                                      uint64_t* key_hash, int32_t* permits, int64_t* now_ns,
                                      uint16_t* limiter, void* stream) {

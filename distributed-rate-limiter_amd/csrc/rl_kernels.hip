@@ -1794,6 +1794,79 @@ __global__ __launch_bounds__(256) void k_route_unpack(uint32_t n, const uint32_t
     remaining[i] = v >> 1;
 }
 
+// Compact wire: 16 B per request in owner order. wire[2j] = key hash, wire[2j+1] =
+// permits (as u32) << 32 | (now_ms - base_ms). base_ms = floor(now_ns[0] / 1e6) - 2^31 of
+// this source's batch, so any batch spanning < 2^31 ms each side of its first request is
+// exact; hdr[1] flags a request outside that range (the router then sends this step in
+// the wide layout). The engine floors now_ns to ms, so nothing it reads is lost.
+__global__ __launch_bounds__(256) void k_route_pack_wire(uint32_t n, const uint32_t* __restrict__ perm,
+                                                         const uint64_t* __restrict__ key,
+                                                         const int32_t* __restrict__ permits,
+                                                         const int64_t* __restrict__ now,
+                                                         const uint16_t* __restrict__ lim,
+                                                         uint64_t* __restrict__ wire,
+                                                         uint16_t* __restrict__ lim_o,
+                                                         int64_t* __restrict__ hdr) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t base = floor_div_ms(now[0]) - (1LL << 31);
+    if (j == 0) hdr[0] = base;
+    bool bad = false;
+    if (j < n) {
+        const uint32_t i = perm[j];
+        const int64_t rel = floor_div_ms(now[i]) - base;
+        bad = rel < 0 || rel > 0xFFFFFFFFLL;
+        ulonglong2 w;
+        w.x = key[i];
+        w.y = (uint64_t)(uint32_t)permits[i] << 32 | (uint64_t)(uint32_t)rel;
+        *(ulonglong2*)(wire + 2 * (size_t)j) = w;
+        if (lim_o) lim_o[j] = lim ? lim[i] : 0;
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&hdr[1], 1ULL);
+}
+
+struct WireSrc {                 // receiver: source s holds requests [end[s-1], end[s])
+    int64_t base[kMaxShards];
+    uint32_t end[kMaxShards];
+    uint32_t n_src;
+};
+
+__global__ __launch_bounds__(256) void k_route_unwire(uint32_t m, const uint64_t* __restrict__ wire,
+                                                      WireSrc src, uint64_t* __restrict__ key_o,
+                                                      int32_t* __restrict__ permits_o,
+                                                      int64_t* __restrict__ now_o) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    uint32_t s = 0;
+    while (s + 1 < src.n_src && j >= src.end[s]) ++s;
+    const ulonglong2 w = *(const ulonglong2*)(wire + 2 * (size_t)j);
+    key_o[j] = w.x;
+    permits_o[j] = (int32_t)(uint32_t)(w.y >> 32);
+    now_o[j] = (src.base[s] + (int64_t)(uint32_t)w.y) * 1000000LL;
+}
+
+// Decisions travel back in the engine's packed-result width W (1 B for max <= 124):
+// ((remaining + 3) << 1) | allowed, as pack_result.
+template <class W>
+__global__ __launch_bounds__(256) void k_route_fold_w(uint32_t n, const uint8_t* __restrict__ allowed,
+                                                      const int64_t* __restrict__ remaining,
+                                                      W* __restrict__ packed) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) packed[j] = (W)pack_result(allowed[j] & 1u, remaining[j]);
+}
+
+template <class W>
+__global__ __launch_bounds__(256) void k_route_unpack_w(uint32_t n, const uint32_t* __restrict__ perm,
+                                                        const W* __restrict__ packed,
+                                                        uint8_t* __restrict__ allowed,
+                                                        int64_t* __restrict__ remaining) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t v = (uint64_t)packed[j];
+    const uint32_t i = perm[j];
+    allowed[i] = (uint8_t)(v & 1u);
+    remaining[i] = (int64_t)(v >> 1) - kResBias;
+}
+
 // ------------------------------------------------------------------ launchers
 static inline uint32_t tiles_for(uint32_t n) { return (n + kTile - 1) / kTile; }
 
@@ -1996,6 +2069,58 @@ hipError_t launch_route_unpack(uint32_t n, const uint32_t* perm, const int64_t* 
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_route_unpack, dim3((n + 255) / 256), dim3(256), 0, s, n, perm, packed,
                        allowed, remaining);
+    return hipGetLastError();
+}
+
+
+hipError_t launch_route_pack_wire(uint32_t n, const uint32_t* perm, const uint64_t* key,
+                                  const int32_t* permits, const int64_t* now, const uint16_t* lim,
+                                  uint64_t* wire, uint16_t* lim_o, int64_t* hdr, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(hdr, 0, 2 * sizeof(int64_t), s);
+    if (e != hipSuccess || n == 0) return e;
+    hipLaunchKernelGGL(k_route_pack_wire, dim3((n + 255) / 256), dim3(256), 0, s, n, perm, key,
+                       permits, now, lim, wire, lim_o, hdr);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_unwire(uint32_t m, const uint64_t* wire, uint32_t n_src, const int64_t* base,
+                               const uint32_t* end, uint64_t* key_o, int32_t* permits_o,
+                               int64_t* now_o, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    if (n_src == 0 || n_src > (uint32_t)kMaxShards) return hipErrorInvalidValue;
+    WireSrc src{};
+    for (uint32_t i = 0; i < n_src; ++i) { src.base[i] = base[i]; src.end[i] = end[i]; }
+    src.n_src = n_src;
+    hipLaunchKernelGGL(k_route_unwire, dim3((m + 255) / 256), dim3(256), 0, s, m, wire, src, key_o,
+                       permits_o, now_o);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_fold_w(uint32_t n, const uint8_t* allowed, const int64_t* remaining,
+                               void* packed, int width, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const dim3 g((n + 255) / 256), b(256);
+    switch (width) {
+    case 1: hipLaunchKernelGGL(k_route_fold_w<uint8_t>, g, b, 0, s, n, allowed, remaining, (uint8_t*)packed); break;
+    case 2: hipLaunchKernelGGL(k_route_fold_w<uint16_t>, g, b, 0, s, n, allowed, remaining, (uint16_t*)packed); break;
+    case 4: hipLaunchKernelGGL(k_route_fold_w<uint32_t>, g, b, 0, s, n, allowed, remaining, (uint32_t*)packed); break;
+    case 8: hipLaunchKernelGGL(k_route_fold_w<uint64_t>, g, b, 0, s, n, allowed, remaining, (uint64_t*)packed); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_route_unpack_w(uint32_t n, const uint32_t* perm, const void* packed, int width,
+                                 uint8_t* allowed, int64_t* remaining, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const dim3 g((n + 255) / 256), b(256);
+    switch (width) {
+    case 1: hipLaunchKernelGGL(k_route_unpack_w<uint8_t>, g, b, 0, s, n, perm, (const uint8_t*)packed, allowed, remaining); break;
+    case 2: hipLaunchKernelGGL(k_route_unpack_w<uint16_t>, g, b, 0, s, n, perm, (const uint16_t*)packed, allowed, remaining); break;
+    case 4: hipLaunchKernelGGL(k_route_unpack_w<uint32_t>, g, b, 0, s, n, perm, (const uint32_t*)packed, allowed, remaining); break;
+    case 8: hipLaunchKernelGGL(k_route_unpack_w<uint64_t>, g, b, 0, s, n, perm, (const uint64_t*)packed, allowed, remaining); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -94,6 +94,7 @@ struct RegionArgs {
                                // {t_start, t_end, records, rounds, 4 x cycle counters}
 };
 
+constexpr int kMaxShards = 64;              // routing: shards per router
 constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
 constexpr uint32_t kDbgWords = 8;        // debug words per bin
@@ -186,5 +187,15 @@ hipError_t launch_route_fold(uint32_t n, const uint8_t* allowed, const int64_t* 
                              int64_t* packed, hipStream_t s);
 hipError_t launch_route_unpack(uint32_t n, const uint32_t* perm, const int64_t* packed,
                                uint8_t* allowed, int64_t* remaining, hipStream_t s);
+hipError_t launch_route_pack_wire(uint32_t n, const uint32_t* perm, const uint64_t* key,
+                                  const int32_t* permits, const int64_t* now, const uint16_t* lim,
+                                  uint64_t* wire, uint16_t* lim_o, int64_t* hdr, hipStream_t s);
+hipError_t launch_route_unwire(uint32_t m, const uint64_t* wire, uint32_t n_src, const int64_t* base,
+                               const uint32_t* end, uint64_t* key_o, int32_t* permits_o,
+                               int64_t* now_o, hipStream_t s);
+hipError_t launch_route_fold_w(uint32_t n, const uint8_t* allowed, const int64_t* remaining,
+                               void* packed, int width, hipStream_t s);
+hipError_t launch_route_unpack_w(uint32_t n, const uint32_t* perm, const void* packed, int width,
+                                 uint8_t* allowed, int64_t* remaining, hipStream_t s);
 
 }  // namespace rl

@@ -40,6 +40,8 @@ EXPORTS = [
     "rl_batch_stats_get", "rl_stage_times", "rl_sync", "rl_strerror", "rl_abi_version",
     "rl_owner_of", "rl_route_partition", "rl_synth_trace_device", "rl_tune",
     "rl_route_pack", "rl_route_fold", "rl_route_unpack", "rl_debug_fetch",
+    "rl_route_pack_wire", "rl_route_unwire", "rl_result_width", "rl_route_fold_packed",
+    "rl_route_unpack_packed",
 ]
 
 
@@ -128,6 +130,11 @@ def lib():
     L.rl_route_pack.argtypes = [vp, sz] + [vp] * 10
     L.rl_route_fold.argtypes = [vp, sz] + [vp] * 4
     L.rl_route_unpack.argtypes = [vp, sz] + [vp] * 5
+    L.rl_route_pack_wire.argtypes = [vp, sz] + [vp] * 9
+    L.rl_route_unwire.argtypes = [vp, sz, vp, u32, vp, vp, vp, vp, vp, vp]
+    L.rl_result_width.argtypes = [vp]
+    L.rl_route_fold_packed.argtypes = [vp, sz, vp, vp, vp, ctypes.c_int, vp]
+    L.rl_route_unpack_packed.argtypes = [vp, sz, vp, vp, ctypes.c_int, vp, vp, vp]
     L.rl_debug_fetch.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.rl_synth_trace_device.argtypes = [vp, ctypes.POINTER(TraceSpec), sz, vp, vp, vp, vp, vp]
     _lib = L
@@ -318,6 +325,41 @@ class Engine:
                                      _p(stream))
         if st != RL_OK:
             raise RlError(st, "rl_route_unpack")
+
+    def route_pack_wire(self, n, perm, key, permits, now, limiter, wire_o, limiter_o, hdr,
+                        stream=None):
+        st = self._L.rl_route_pack_wire(self._h, n, _p(perm), _p(key), _p(permits), _p(now),
+                                        _p(limiter), _p(wire_o), _p(limiter_o), _p(hdr),
+                                        _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_pack_wire")
+
+    def route_unwire(self, m, wire, src_base, src_count, key_o, permits_o, now_o, stream=None):
+        base = np.ascontiguousarray(src_base, dtype=np.int64)
+        cnt = np.ascontiguousarray(src_count, dtype=np.uint64)
+        st = self._L.rl_route_unwire(self._h, m, _p(wire), len(base), base.ctypes.data,
+                                     cnt.ctypes.data, _p(key_o), _p(permits_o), _p(now_o),
+                                     _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_unwire")
+
+    def result_width(self):
+        w = self._L.rl_result_width(self._h)
+        if w < 0:
+            raise RlError(w, "rl_result_width")
+        return w
+
+    def route_fold_packed(self, n, allowed, remaining, packed, width, stream=None):
+        st = self._L.rl_route_fold_packed(self._h, n, _p(allowed), _p(remaining), _p(packed),
+                                          width, _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_fold_packed")
+
+    def route_unpack_packed(self, n, perm, packed, width, allowed, remaining, stream=None):
+        st = self._L.rl_route_unpack_packed(self._h, n, _p(perm), _p(packed), width, _p(allowed),
+                                            _p(remaining), _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_unpack_packed")
 
     def synth_trace(self, n, keys, permits, now_ns, limiter, *, seed, n_keys, dist=DIST_UNIFORM,
                     zipf_s=1.1, permits_max=4, t0_ns=1_700_000_000_000 * 1_000_000,

@@ -205,6 +205,30 @@ int  rl_route_fold(rl_engine* e, size_t n, const uint8_t* allowed, const int64_t
 int  rl_route_unpack(rl_engine* e, size_t n, const uint32_t* perm, const int64_t* packed,
                      uint8_t* allowed, int64_t* remaining, void* stream);
 
+/* Compact wire (16 B per request, the default router layout): out in owner order,
+ * wire_out[2j] = key_hash, wire_out[2j+1] = (uint32)permits << 32 | (now_ms - base_ms),
+ * limiter_out[j] (nullable) = limiter id. hdr (device int64[2]) receives base_ms =
+ * floorDiv(now_ns[0], 1e6) - 2^31 and an overflow flag (1: some now_ms outside
+ * [base_ms, base_ms + 2^32); the router then sends that step in the wide layout). */
+int  rl_route_pack_wire(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key_hash,
+                        const int32_t* permits, const int64_t* now_ns, const uint16_t* limiter,
+                        uint64_t* wire_out, uint16_t* limiter_out, int64_t* hdr, void* stream);
+/* Receiver side: m wire records from n_src sources (host arrays: each source's base_ms
+ * and request count, in source order, summing to m) -> request SoA for the engine
+ * (now_out = now_ms * 1e6; the engine reads now at ms resolution). */
+int  rl_route_unwire(rl_engine* e, size_t m, const uint64_t* wire, uint32_t n_src,
+                     const int64_t* src_base, const uint64_t* src_count, uint64_t* key_out,
+                     int32_t* permits_out, int64_t* now_out, void* stream);
+/* Width in bytes (1, 2, 4 or 8) of the engine's packed decision ((remaining + 3) << 1 |
+ * allowed) for its current limiter set: 1 B for every maxPermits <= 124. */
+int  rl_result_width(rl_engine* e);
+/* packed[j] = (remaining[j] + 3) << 1 | allowed[j] in `width` bytes (return trip), and
+ * its inverse scattered through perm: allowed[perm[j]], remaining[perm[j]]. */
+int  rl_route_fold_packed(rl_engine* e, size_t n, const uint8_t* allowed, const int64_t* remaining,
+                          void* packed, int width, void* stream);
+int  rl_route_unpack_packed(rl_engine* e, size_t n, const uint32_t* perm, const void* packed,
+                            int width, uint8_t* allowed, int64_t* remaining, void* stream);
+
 /* ---- synthetic traces (bench / tests; deterministic in (seed, index)) ------ */
 #define RL_DIST_UNIFORM 0
 #define RL_DIST_ZIPF    1

@@ -28,7 +28,7 @@ def _trace(steps, world, n):
     return keys, permits, now, lim
 
 
-def _worker(rank, world, port, steps, n, out):
+def _worker(rank, world, port, steps, n, out, lims):
     import rl_amd
     from rl_amd.router import DeviceOps, Router
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -37,9 +37,10 @@ def _worker(rank, world, port, steps, n, out):
     dev = torch.device("cuda", 0)
     eng = rl_amd.Engine(device=0, max_batch=4 * n, capacity=1 << 16, shard_index=rank,
                         shard_count=world)
-    eng.add_limiter(rl_amd.TB, 50, 60000, 10.0)
-    eng.add_limiter(rl_amd.SW, 30, 5000, 0.0)
-    router = Router(DeviceOps(eng, world, dev, n), world, rank, exchange_device="cpu")
+    for l in lims:
+        eng.add_limiter(*l)
+    ops = DeviceOps(eng, world, dev, n)
+    router = Router(ops, world, rank, exchange_device="cpu")
     keys, permits, now, lim = _trace(steps, world, n)
     res_a, res_r = [], []
     for s in range(steps):
@@ -55,11 +56,17 @@ def _worker(rank, world, port, steps, n, out):
         res_a.append(a.cpu().numpy())
         res_r.append(r.cpu().numpy())
     assert eng.last_status() == rl_amd.RL_OK
+    top = (max(l[1] for l in lims) + 3) * 2 + 1
+    assert ops.result_width() == (1 if top < 256 else 2 if top < 65536 else 4)
     np.savez(f"{out}.{rank}.npz", a=np.concatenate(res_a), r=np.concatenate(res_r))
     dist.destroy_process_group()
 
 
-def test_two_shards_one_gpu(tmp_path):
+@pytest.mark.parametrize("lims,width", [
+    ([[1, 50, 60000, 10.0], [0, 30, 5000, 0.0]], 1),           # decisions return as 1 B
+    ([[1, 500, 60000, 10.0], [0, 40000, 5000, 0.0]], 4),       # ... and as 4 B
+])
+def test_two_shards_one_gpu(tmp_path, lims, width):
     from oracle.coracle import COracle
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -67,9 +74,11 @@ def test_two_shards_one_gpu(tmp_path):
     s.close()
     world, steps, n = 2, 3, 100_000
     out = str(tmp_path / "r")
-    mp.spawn(_worker, args=(world, port, steps, n, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, steps, n, out, lims), nprocs=world, join=True)
     keys, permits, now, lim = _trace(steps, world, n)
-    wa, wr, _, _ = COracle([[1, 50, 60000, 10.0], [0, 30, 5000, 0.0]]).run(
+    top = (max(l[1] for l in lims) + 3) * 2 + 1
+    assert width == (1 if top < 256 else 2 if top < 65536 else 4)
+    wa, wr, _, _ = COracle(lims).run(
         keys, permits, now, lim, want_tokens=False)
     for rank in range(world):
         d = np.load(f"{out}.{rank}.npz")
@@ -77,3 +86,45 @@ def test_two_shards_one_gpu(tmp_path):
             sl = slice((st * world + rank) * n, (st * world + rank + 1) * n)
             assert np.array_equal(d["a"][st * n:(st + 1) * n], wa[sl])
             assert np.array_equal(d["r"][st * n:(st + 1) * n], wr[sl])
+
+
+def test_wire_pack_unwire_roundtrip():
+    """k_route_pack_wire -> k_route_unwire restores key, permits and now at ms resolution
+    (negative permits and sub-ms now included), and flags a span past 2^31 ms."""
+    import rl_amd
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    eng = rl_amd.Engine(device=0, max_batch=1 << 12, capacity=1 << 12)
+    eng.add_limiter(rl_amd.TB, 50, 60000, 10.0)
+    rng = np.random.default_rng(3)
+    n = 5000
+    keys = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+    permits = rng.integers(-5, 2**31 - 1, n).astype(np.int32)
+    now = (T0 * NS + rng.integers(-2**30 * NS, 2**30 * NS, n)).astype(np.int64)
+    perm = rng.permutation(n).astype(np.int32)
+    td = lambda x: torch.from_numpy(x).to(dev)
+    wire = torch.empty((n, 2), dtype=torch.int64, device=dev)
+    hdr = torch.empty(2, dtype=torch.int64, device=dev)
+    eng.route_pack_wire(n, td(perm), td(keys), td(permits), td(now), None, wire, None, hdr)
+    eng.sync()
+    base, ovf = hdr.cpu().tolist()
+    assert base == now[0] // NS - 2**31 and ovf == 0
+    k = torch.empty(n, dtype=torch.int64, device=dev)
+    p = torch.empty(n, dtype=torch.int32, device=dev)
+    t = torch.empty(n, dtype=torch.int64, device=dev)
+    split = [1234, n - 1234]                       # two sources with different bases
+    eng.route_unwire(n, wire, [base, base], split, k, p, t)
+    eng.sync()
+    assert np.array_equal(k.cpu().numpy(), keys[perm])
+    assert np.array_equal(p.cpu().numpy(), permits[perm])
+    assert np.array_equal(t.cpu().numpy() // NS, now[perm] // NS)
+    eng.route_unwire(n, wire, [base, base + 7], split, k, p, t)
+    eng.sync()
+    got = t.cpu().numpy() // NS
+    assert np.array_equal(got[:1234], now[perm][:1234] // NS)
+    assert np.array_equal(got[1234:], now[perm][1234:] // NS + 7)
+    now2 = now.copy()
+    now2[-1] = now[0] + (2**31 + 5) * NS                   # beyond the 32-bit wire time
+    eng.route_pack_wire(n, td(perm), td(keys), td(permits), td(now2), None, wire, None, hdr)
+    eng.sync()
+    assert hdr.cpu().tolist()[1] == 1
