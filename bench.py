@@ -149,10 +149,18 @@ def main():
     ws, rank, local = dist_env()
     if ws != args.gpus and not (ws == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    # RL_BENCH_REHEARSE=1: every rank on cuda:0, exchanges through gloo on the host — a
+    # functional rehearsal of the N>1 path on a one-GPU box (its numbers mean nothing)
+    rehearse = ws > 1 and os.environ.get("RL_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = CONFIGS[args.config]
     n = args.batch or cfg["batch"]
     steps, warm = args.steps, args.warmup
@@ -192,7 +200,8 @@ def main():
 
     if ws > 1:
         from rl_amd.router import DeviceOps, Router
-        router = Router(DeviceOps(eng, ws, dev, n), ws, rank)
+        router = Router(DeviceOps(eng, ws, dev, n), ws, rank,
+                        exchange_device="cpu" if rehearse else None)
 
         def step(s):
             k, p, t, li = inputs[s]
@@ -223,7 +232,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if ws > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     st = eng.last_status()
