@@ -466,14 +466,15 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     mark(e, 6);
     if (passes == 2) {
-        // bin boundaries from the final order (no per-request atomics: a hot bin would
-        // serialise them)
-        HIP_OK(hipMemsetAsync(e->region_start, 0, (size_t)n_bins * sizeof(uint32_t), s));
-        HIP_OK(hipMemsetAsync(e->region_count, 0, (size_t)n_bins * sizeof(uint32_t), s));
+        // bin boundaries of the final order: binary searches inside the high-digit runs
+        // that pass 1's scan delimits (no per-request atomics: a hot bin would serialise
+        // them; no full read of the records)
         BoundsArgs ba{};
         ba.rec = rec_final; ba.n = (uint32_t)n; ba.n_lim = (uint32_t)e->lims.size();
         ba.lims = e->d_lims; ba.shard_bits = e->shard_bits; ba.bin_shift = bsh;
         ba.rstart = e->region_start; ba.rend = e->region_count;
+        ba.hi_base = e->bin_base; ba.hi_total = e->bin_total;
+        ba.n_bins = n_bins; ba.d0 = d0; ba.d1 = d1;
         HIP_OK(launch_bin_bounds(ba, wide, s));
         rstart = e->region_start;
         rcount = nullptr;

@@ -1501,31 +1501,47 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
 }
 
 // Bin boundaries of the final record order (two-pass partitions): rstart[b] / rend[b]
-// for every bin that holds records (both arrays zeroed before, so empty bins read 0).
+// for every bin b < n_bins. The high-digit pass leaves run hi = [hi_base[hi],
+// hi_base[hi] + hi_total[hi]) whose records are still in low-digit order (the pass is
+// stable over the low-digit pass's output), so each low digit's first record is a
+// binary search inside its run: one workgroup per run, ~log2(run) record probes per
+// bin instead of reading every record of the batch.
 template <class Codec>
 __global__ __launch_bounds__(256) void k_bin_bounds(BoundsArgs a) {
     __shared__ uint32_t s_base[256];
     __shared__ uint8_t s_bits[256];
+    __shared__ uint32_t s_lb[(1u << kMaxDigitBits) + 1];
     for (uint32_t l = threadIdx.x; l < a.n_lim; l += 256) {
         s_base[l] = a.lims[l].region_base;
         s_bits[l] = (uint8_t)a.lims[l].region_bits;
     }
     __syncthreads();
     const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
-    auto bin = [&](uint32_t i) {
+    const uint32_t nlo = 1u << a.d0, lo_mask = nlo - 1;
+    auto lo_of = [&](uint32_t i) {
         const typename Codec::Rec r = recs[i];
         const uint32_t lim = Codec::limiter_of(r);
-        return (s_base[lim] + region_local(r.h, a.shard_bits, s_bits[lim])) >> a.bin_shift;
+        return ((s_base[lim] + region_local(r.h, a.shard_bits, s_bits[lim])) >> a.bin_shift) & lo_mask;
     };
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t b = i < a.n ? bin(i) : kNone;
-    uint32_t bp = __shfl_up(b, 1, 64), bn = __shfl_down(b, 1, 64);
-    if (lane == 0) bp = (i > 0 && i - 1 < a.n) ? bin(i - 1) : kNone;
-    if (lane == 63) bn = i + 1 < a.n ? bin(i + 1) : kNone;
-    if (i < a.n) {
-        if (b != bp) a.rstart[b] = i;
-        if (b != bn) a.rend[b] = i + 1;
+    const uint32_t hi = blockIdx.x;
+    const uint32_t beg = a.hi_base[hi], end = beg + a.hi_total[hi];
+    for (uint32_t lo = threadIdx.x; lo <= nlo; lo += 256) {
+        uint32_t L = beg, R = end;                    // first record with low digit >= lo
+        if (lo == nlo) L = end;
+        while (L < R) {
+            const uint32_t m = L + (R - L) / 2;
+            if (lo_of(m) < lo) L = m + 1;
+            else R = m;
+        }
+        s_lb[lo] = L;
+    }
+    __syncthreads();
+    for (uint32_t lo = threadIdx.x; lo < nlo; lo += 256) {
+        const uint32_t b = (hi << a.d0) | lo;
+        if (b < a.n_bins) {
+            a.rstart[b] = s_lb[lo];
+            a.rend[b] = s_lb[lo + 1];
+        }
     }
 }
 
@@ -1987,8 +2003,9 @@ hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, con
 }
 
 hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s) {
-    if (a.n == 0) return hipSuccess;
-    const dim3 g((a.n + 255) / 256), b(256);
+    if (a.n_bins == 0 || a.d0 > kMaxDigitBits || a.d1 > kMaxDigitBits || a.d0 < 1)
+        return hipErrorInvalidValue;
+    const dim3 g(1u << a.d1), b(256);
     if (wide) hipLaunchKernelGGL(k_bin_bounds<CodecW>, g, b, 0, s, a);
     else hipLaunchKernelGGL(k_bin_bounds<CodecC>, g, b, 0, s, a);
     return hipGetLastError();

@@ -118,8 +118,13 @@ struct BoundsArgs {
     const DevLimiter* lims;
     int32_t shard_bits;
     int32_t bin_shift;
-    uint32_t* rstart;          // [bins], zeroed before
-    uint32_t* rend;            // [bins], zeroed before
+    uint32_t* rstart;          // [n_bins]
+    uint32_t* rend;            // [n_bins]
+    const uint32_t* hi_base;   // [2^d1] first record of each high-digit run (pass-1 scan)
+    const uint32_t* hi_total;  // [2^d1] records in each high-digit run
+    uint32_t n_bins;
+    int32_t d0;                // low-digit bits (pass 0)
+    int32_t d1;                // high-digit bits (pass 1)
 };
 
 struct UnpermArgs {
