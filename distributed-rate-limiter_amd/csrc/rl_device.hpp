@@ -42,9 +42,15 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 // Partition tiles (upsweep / scatter / unpermute all share this tiling). 64K
 // requests per tile; grids are persistent (one workgroup per CU) and walk the tiles
 // so that the 32 workgroups of an XCD work on 32 consecutive tiles at a time.
-constexpr int kTileThreads = 256;
-constexpr int kTileItems = 256;
-constexpr int kTile = kTileThreads * kTileItems;  // 65536 requests per tile
+#ifndef RL_TILE_THREADS
+#define RL_TILE_THREADS 256
+#endif
+constexpr int kTileThreads = RL_TILE_THREADS;
+#ifndef RL_TILE_ITEMS
+#define RL_TILE_ITEMS 256                          // per-thread items per tile (A/B builds: -DRL_TILE_ITEMS)
+#endif
+constexpr int kTileItems = RL_TILE_ITEMS;
+constexpr int kTile = kTileThreads * kTileItems;  // 65536 requests per tile (default)
 constexpr int kMaxDigitBits = 13;                 // <= 8192 bins per pass
 
 // Compact record field limits.

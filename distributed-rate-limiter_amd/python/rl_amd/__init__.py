@@ -14,7 +14,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REPO = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "librl_engine.so")
+LIB_PATH = os.environ.get("RL_ENGINE_LIB") or os.path.join(PKG_DIR, "librl_engine.so")  # A/B builds only
 HEADER = os.path.join(REPO, "include", "rl_engine.h")
 
 RL_OK = 0
