@@ -94,6 +94,16 @@ __host__ __device__ inline uint64_t mix64(uint64_t x) {
     return x;
 }
 
+// Inverse of mix64 (state export recovers key_hash from a slot's tag).
+__host__ __device__ inline uint64_t unmix64(uint64_t x) {
+    x ^= (x >> 31) ^ (x >> 62);
+    x *= 0x319642b2d24d8ec3ULL;          // 0x94d049bb133111eb^-1 mod 2^64
+    x ^= (x >> 27) ^ (x >> 54);
+    x *= 0x96de1b173f119089ULL;          // 0xbf58476d1ce4e5b9^-1 mod 2^64
+    x ^= (x >> 30) ^ (x >> 60);
+    return x;
+}
+
 // owner shard = top s bits of h; region = next k bits.
 __host__ __device__ inline uint32_t region_local(uint64_t h, int shard_bits, int k) {
     if (k == 0) return 0;

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -886,4 +887,173 @@ extern "C" int rl_debug_fetch(rl_engine* e, const char* what, void* out, size_t 
         return (int)(nb / (kDbgWords * sizeof(uint64_t)));
     }
     return RL_E_INVALID_ARG;
+}
+
+// ---------------------------------------------------------------- state export / import
+// the engine's state in the reference's Redis keyspace layout
+// (SlidingWindowRateLimiter.java:185-188 + RedisRateLimitStorage.java:38-49;
+// TokenBucketRateLimiter.java:46-48,63-64).
+static_assert(sizeof(StateRec) == sizeof(rl_state_entry), "StateRec layout");
+static_assert(offsetof(StateRec, expire_at_ms) == offsetof(rl_state_entry, expire_at_ms), "StateRec layout");
+
+extern "C" int rl_export_state(rl_engine* e, int64_t now_ns, rl_state_entry* out, size_t cap,
+                               size_t* n_out) {
+    if (!e || !n_out || (cap && !out)) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    const int64_t now = floor_div_ms(now_ns);
+    const uint32_t dcap = (uint32_t)std::min<size_t>(cap, 0xFFFFFFF0u);
+    StateRec* d_out = nullptr;
+    uint32_t* d_count = nullptr;
+    if (dalloc(&d_out, std::max<uint32_t>(dcap, 1u)) != RL_OK) return RL_E_NOMEM;
+    if (dalloc(&d_count, e->lims.size() + 1) != RL_OK) { dfree(d_out); return RL_E_NOMEM; }
+    int rc = RL_OK;
+    uint32_t total = 0;
+    if (hipMemsetAsync(d_count, 0, sizeof(uint32_t), e->stream) != hipSuccess) rc = RL_E_DEVICE;
+    for (size_t li = 0; rc == RL_OK && li < e->lims.size(); ++li) {
+        const HostLimiter& h = e->lims[li];
+        if (launch_export((const Slot*)h.table, h.table_bytes / sizeof(Slot), h.dev, (uint16_t)li,
+                          now, d_out, dcap, d_count, e->stream) != hipSuccess)
+            rc = RL_E_DEVICE;
+    }
+    if (rc == RL_OK && (hipMemcpyAsync(&total, d_count, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                       e->stream) != hipSuccess ||
+                        hipStreamSynchronize(e->stream) != hipSuccess))
+        rc = RL_E_DEVICE;
+    if (rc == RL_OK) {
+        *n_out = total;
+        if (total > cap) {
+            rc = RL_E_TOO_LARGE;
+        } else if (total) {
+            if (hipMemcpy(out, d_out, (size_t)total * sizeof(StateRec), hipMemcpyDeviceToHost) != hipSuccess) {
+                rc = RL_E_DEVICE;
+            } else {
+                std::sort(out, out + total, [](const rl_state_entry& x, const rl_state_entry& y) {
+                    if (x.limiter != y.limiter) return x.limiter < y.limiter;
+                    if (x.key_hash != y.key_hash) return x.key_hash < y.key_hash;
+                    return x.window_start_ms < y.window_start_ms;
+                });
+            }
+        }
+    }
+    dfree(d_out);
+    dfree(d_count);
+    return rc;
+}
+
+extern "C" int rl_import_state(rl_engine* e, const rl_state_entry* in, size_t n, size_t* n_imported) {
+    if (!e || (n && !in)) return RL_E_INVALID_ARG;
+    if (n_imported) *n_imported = 0;
+    if (n == 0) return RL_OK;
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    std::vector<const rl_state_entry*> v(n);
+    for (size_t i = 0; i < n; ++i) {
+        const rl_state_entry& x = in[i];
+        if (x.limiter >= e->lims.size()) return RL_E_INVALID_ARG;
+        const DevLimiter& L = e->lims[x.limiter].dev;
+        if (x.kind != (L.algo == kAlgoTB ? RL_STATE_TB_BUCKET : RL_STATE_SW_BUCKET)) return RL_E_INVALID_ARG;
+        if (L.algo == kAlgoTB) {
+            if (x.expire_at_ms != x.last_refill_ms + L.ttl_ms) return RL_E_INVALID_ARG;
+        } else {
+            const int64_t w = L.window_ms;
+            if (x.count < 1 || x.count > 0xFFFFFFFFLL || x.window_start_ms % w != 0) return RL_E_INVALID_ARG;
+            const int64_t off = x.expire_at_ms - w - x.window_start_ms;   // last INCR - W
+            if (off < 0 || off >= w) return RL_E_INVALID_ARG;
+        }
+        v[i] = &x;
+    }
+    // (limiter, key) groups, newest bucket first
+    std::sort(v.begin(), v.end(), [](const rl_state_entry* x, const rl_state_entry* y) {
+        if (x->limiter != y->limiter) return x->limiter < y->limiter;
+        if (x->key_hash != y->key_hash) return x->key_hash < y->key_hash;
+        return x->window_start_ms > y->window_start_ms;
+    });
+    struct Img { uint64_t addr; uint8_t algo; Slot s; };
+    std::vector<Img> imgs;
+    size_t taken = 0;
+    for (size_t i = 0; i < n;) {
+        size_t j = i + 1;
+        while (j < n && v[j]->limiter == v[i]->limiter && v[j]->key_hash == v[i]->key_hash) ++j;
+        const rl_state_entry& x = *v[i];
+        const HostLimiter& h = e->lims[x.limiter];
+        const DevLimiter& L = h.dev;
+        const uint64_t tag = mix64(x.key_hash);
+        const bool mine = e->opts.shard_count <= 1 ||
+                          (uint32_t)(tag >> (64 - e->shard_bits)) == e->opts.shard_index;
+        if (mine) {
+            Img im{};
+            im.algo = (uint8_t)L.algo;
+            im.s.tag = tag;
+            if (L.algo == kAlgoTB) {                   // one hash per key: the first one wins
+                uint64_t bits;
+                std::memcpy(&bits, &x.tokens, 8);
+                im.s.a = bits; im.s.b = (uint64_t)x.last_refill_ms; im.s.c = 1;
+                taken += 1;
+            } else {
+                const int64_t w = L.window_ms;
+                int64_t b1 = x.window_start_ms;
+                uint64_t c1 = (uint64_t)x.count, c0 = 0;
+                int64_t o1 = x.expire_at_ms - w - b1, o0 = 0;
+                taken += 1;
+                if (j > i + 1 && v[i + 1]->window_start_ms == b1 - w) {
+                    c0 = (uint64_t)v[i + 1]->count;
+                    o0 = v[i + 1]->expire_at_ms - w - (b1 - w);
+                    taken += 1;
+                }
+                im.s.a = (uint64_t)b1;
+                im.s.b = c1 | (c0 << 32);
+                im.s.c = (uint64_t)(uint32_t)o1 | ((uint64_t)(uint32_t)o0 << 32);
+            }
+            const uint32_t region = region_local(tag, e->shard_bits, L.region_bits);
+            im.addr = (uint64_t)(uintptr_t)h.table + (uint64_t)region * kRegionSlots * sizeof(Slot);
+            imgs.push_back(im);
+        }
+        i = j;
+    }
+    if (imgs.empty()) return RL_OK;
+    std::stable_sort(imgs.begin(), imgs.end(), [](const Img& x, const Img& y) { return x.addr < y.addr; });
+    std::vector<uint32_t> off;
+    std::vector<uint64_t> addr;
+    std::vector<uint8_t> algo;
+    std::vector<Slot> slots(imgs.size());
+    for (size_t k = 0; k < imgs.size(); ++k) {
+        if (k == 0 || imgs[k].addr != imgs[k - 1].addr) {
+            off.push_back((uint32_t)k);
+            addr.push_back(imgs[k].addr);
+            algo.push_back(imgs[k].algo);
+        }
+        slots[k] = imgs[k].s;
+    }
+    off.push_back((uint32_t)imgs.size());
+    const size_t G = addr.size();
+    const size_t bytes = slots.size() * sizeof(Slot) + G * 8 + (G + 1) * 4 + G + 16;
+    uint8_t* d = nullptr;
+    if (dalloc(&d, bytes) != RL_OK) return RL_E_NOMEM;
+    Slot* d_img = (Slot*)d;
+    uint64_t* d_addr = (uint64_t*)(d + slots.size() * sizeof(Slot));
+    uint32_t* d_off = (uint32_t*)(d_addr + G);
+    uint32_t* d_fail = d_off + G + 1;
+    uint8_t* d_algo = (uint8_t*)(d_fail + 1);
+    int rc = RL_OK;
+    uint32_t fail = 0;
+    if (hipMemcpyAsync(d_img, slots.data(), slots.size() * sizeof(Slot), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipMemcpyAsync(d_addr, addr.data(), G * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipMemcpyAsync(d_off, off.data(), (G + 1) * 4, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipMemcpyAsync(d_algo, algo.data(), G, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipMemsetAsync(d_fail, 0, 4, e->stream) != hipSuccess)
+        rc = RL_E_DEVICE;
+    if (rc == RL_OK) {
+        ImportArgs a{};
+        a.n_groups = (uint32_t)G; a.group_off = d_off; a.region_addr = d_addr; a.group_algo = d_algo;
+        a.img = d_img; a.fail = d_fail;
+        if (launch_import(a, e->stream) != hipSuccess ||
+            hipMemcpyAsync(&fail, d_fail, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            rc = RL_E_DEVICE;
+    }
+    (void)hipFree(d);
+    if (rc != RL_OK) return rc;
+    if (n_imported) *n_imported = taken;
+    return fail ? RL_E_CAPACITY : RL_OK;
 }

@@ -1883,6 +1883,102 @@ __global__ __launch_bounds__(256) void k_route_unpack_w(uint32_t n, const uint32
     remaining[i] = (int64_t)(v >> 1) - kResBias;
 }
 
+// ------------------------------------------------------------------ state export / import
+// Export: one thread per slot of one limiter's table; every bucket live at `now` becomes one
+// Redis-layout entry (SW: "rl:<key>:<W>" counters, deadline last INCR + w; TB: "tb:<key>",
+// deadline last_refill + 2w), compacted through one counter. The host sorts the entries.
+__global__ __launch_bounds__(256) void k_export(const Slot* __restrict__ tab, uint64_t n_slots,
+                                                DevLimiter L, uint16_t lim, int64_t now,
+                                                StateRec* __restrict__ out, uint32_t cap,
+                                                uint32_t* count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_slots) return;
+    const Slot v = tab[i];
+    StateRec r[2];
+    int m = 0;
+    const uint64_t key = unmix64(v.tag);
+    if (L.algo == kAlgoTB) {
+        if ((v.c & 1u) && !(now > (int64_t)v.b + L.ttl_ms)) {
+            StateRec& e = r[m++];
+            e = StateRec{};
+            e.key_hash = key; e.limiter = lim; e.kind = 1;
+            e.tokens = __longlong_as_double((long long)v.a);
+            e.last_refill_ms = (int64_t)v.b;
+            e.expire_at_ms = (int64_t)v.b + L.ttl_ms;
+        }
+    } else {
+        const SW2 q = sw_unpack(v.a, v.b, v.c);
+        const int64_t w = L.window_ms;
+        const int64_t d1 = q.b1_start + q.b1_off + w, d0 = q.b1_start + q.b0_off;
+        if (q.b0_cnt != 0 && !(now > d0)) {          // bucket b1_start - w (sorted first)
+            StateRec& e = r[m++];
+            e = StateRec{};
+            e.key_hash = key; e.limiter = lim; e.kind = 0;
+            e.window_start_ms = q.b1_start - w; e.count = q.b0_cnt; e.expire_at_ms = d0;
+        }
+        if (q.b1_cnt != 0 && !(now > d1)) {
+            StateRec& e = r[m++];
+            e = StateRec{};
+            e.key_hash = key; e.limiter = lim; e.kind = 0;
+            e.window_start_ms = q.b1_start; e.count = q.b1_cnt; e.expire_at_ms = d1;
+        }
+    }
+    if (m == 0) return;
+    const uint32_t k = atomicAdd(count, (uint32_t)m);
+    for (int j = 0; j < m; ++j)
+        if (k + (uint32_t)j < cap) out[k + j] = r[j];
+}
+
+// Import: one wave per region that receives entries. The wave stages the region's 256
+// slots in LDS, applies its keys in order (replace the slot holding the key's tag, else
+// claim the first slot whose state is absent), and writes the region back. Regions are
+// rebuilt from their live slots whenever a batch loads them, so any free slot will do.
+__global__ __launch_bounds__(64) void k_import(ImportArgs a) {
+    __shared__ Slot S[kRegionSlots];
+    const uint32_t g = blockIdx.x, lane = threadIdx.x;
+    if (g >= a.n_groups) return;
+    Slot* tab = (Slot*)(uintptr_t)a.region_addr[g];
+    const bool tb = a.group_algo[g] == kAlgoTB;
+    for (uint32_t k = lane; k < kRegionSlots; k += 64) S[k] = tab[k];
+    wave_fence();
+    for (uint32_t j = a.group_off[g]; j < a.group_off[g + 1]; ++j) {
+        const Slot im = a.img[j];
+        uint64_t hit = 0, fre = 0;
+        int32_t first_hit = -1, first_free = -1;
+        for (uint32_t b = 0; b < kRegionSlots / 64; ++b) {
+            const Slot& v = S[b * 64 + lane];
+            const bool absent = tb ? !(v.c & 1u) : v.b == 0;
+            hit = __ballot(v.tag == im.tag);
+            fre = __ballot(absent);
+            if (first_hit < 0 && hit) first_hit = (int32_t)(b * 64 + __builtin_ctzll(hit));
+            if (first_free < 0 && fre) first_free = (int32_t)(b * 64 + __builtin_ctzll(fre));
+        }
+        const int32_t p = first_hit >= 0 ? first_hit : first_free;
+        if (p < 0) {
+            if (lane == 0) atomicAdd(a.fail, 1u);
+        } else if (lane == 0) {
+            S[p] = im;
+        }
+        wave_fence();
+    }
+    for (uint32_t k = lane; k < kRegionSlots; k += 64) tab[k] = S[k];
+}
+
+hipError_t launch_export(const Slot* table, uint64_t n_slots, const DevLimiter& L, uint16_t lim,
+                         int64_t now_ms, StateRec* out, uint32_t cap, uint32_t* count,
+                         hipStream_t s) {
+    const uint64_t blocks = (n_slots + 255) / 256;
+    hipLaunchKernelGGL(k_export, dim3((uint32_t)blocks), dim3(256), 0, s, table, n_slots, L, lim,
+                       now_ms, out, cap, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_import(const ImportArgs& a, hipStream_t s) {
+    if (a.n_groups == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_import, dim3(a.n_groups), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launchers
 static inline uint32_t tiles_for(uint32_t n) { return (n + kTile - 1) / kTile; }
 

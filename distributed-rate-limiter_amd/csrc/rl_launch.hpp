@@ -161,6 +161,31 @@ struct SynthArgs {
     uint64_t n;
 };
 
+// State export / import (rl_export_state / rl_import_state). StateRec has the layout of
+// rl_state_entry (include/rl_engine.h; static_assert in rl_engine.cpp).
+struct StateRec {
+    uint64_t key_hash;
+    uint16_t limiter;
+    uint8_t kind;
+    uint8_t reserved[5];
+    int64_t window_start_ms, count;
+    double tokens;
+    int64_t last_refill_ms, expire_at_ms;
+};
+struct ImportArgs {
+    uint32_t n_groups;
+    const uint32_t* group_off;     // [n_groups + 1] into img
+    const uint64_t* region_addr;   // [n_groups] device address of the region's 256 slots
+    const uint8_t* group_algo;     // [n_groups]
+    const Slot* img;               // slot images, grouped by region
+    uint32_t* fail;                // keys that found no free slot
+};
+
+hipError_t launch_export(const Slot* table, uint64_t n_slots, const DevLimiter& L, uint16_t lim,
+                         int64_t now_ms, StateRec* out, uint32_t cap, uint32_t* count,
+                         hipStream_t s);
+hipError_t launch_import(const ImportArgs& a, hipStream_t s);
+
 hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s);
 hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s);
 hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, uint32_t cols,

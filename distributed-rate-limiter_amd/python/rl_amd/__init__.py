@@ -41,8 +41,14 @@ EXPORTS = [
     "rl_owner_of", "rl_route_partition", "rl_synth_trace_device", "rl_tune",
     "rl_route_pack", "rl_route_fold", "rl_route_unpack", "rl_debug_fetch",
     "rl_route_pack_wire", "rl_route_unwire", "rl_result_width", "rl_route_fold_packed",
-    "rl_route_unpack_packed",
+    "rl_route_unpack_packed", "rl_export_state", "rl_import_state",
 ]
+STATE_SW_BUCKET, STATE_TB_BUCKET = 0, 1
+# rl_state_entry (include/rl_engine.h): one live Redis key ("rl:<key>:<W>" / "tb:<key>")
+STATE_DTYPE = np.dtype([("key_hash", "<u8"), ("limiter", "<u2"), ("kind", "u1"),
+                        ("reserved", "u1", (5,)), ("window_start_ms", "<i8"), ("count", "<i8"),
+                        ("tokens", "<f8"), ("last_refill_ms", "<i8"), ("expire_at_ms", "<i8")])
+assert STATE_DTYPE.itemsize == 56
 
 
 class RlError(RuntimeError):
@@ -137,6 +143,8 @@ def lib():
     L.rl_route_unpack_packed.argtypes = [vp, sz, vp, vp, ctypes.c_int, vp, vp, vp]
     L.rl_debug_fetch.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.rl_synth_trace_device.argtypes = [vp, ctypes.POINTER(TraceSpec), sz, vp, vp, vp, vp, vp]
+    L.rl_export_state.argtypes = [vp, i64, vp, sz, ctypes.POINTER(sz)]
+    L.rl_import_state.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     _lib = L
     return L
 
@@ -269,6 +277,28 @@ class Engine:
         keys = np.ascontiguousarray(keys, np.uint64)
         now_ns = np.ascontiguousarray(now_ns, np.int64)
         return self._L.rl_reset(self._h, int(limiter), keys.shape[0], _p(keys), _p(now_ns))
+
+    def export_state(self, now_ns):
+        """Live state at now_ns in the Redis layout: a STATE_DTYPE array (rl_export_state)."""
+        n = ctypes.c_size_t(0)
+        st = self._L.rl_export_state(self._h, int(now_ns), None, 0, ctypes.byref(n))
+        while True:
+            if st == RL_OK and n.value == 0:
+                return np.zeros(0, STATE_DTYPE)
+            if st not in (RL_OK, RL_E_TOO_LARGE):
+                raise RlError(st, "rl_export_state")
+            out = np.zeros(n.value + 1024, STATE_DTYPE)   # state may grow between calls
+            st = self._L.rl_export_state(self._h, int(now_ns), _p(out), out.shape[0], ctypes.byref(n))
+            if st == RL_OK:
+                return out[:n.value]
+
+    def import_state(self, entries):
+        """Load STATE_DTYPE entries (rl_import_state). Returns (status, entries taken)."""
+        entries = np.ascontiguousarray(entries, STATE_DTYPE)
+        n = ctypes.c_size_t(0)
+        st = self._L.rl_import_state(self._h, _p(entries) if entries.shape[0] else None,
+                                     entries.shape[0], ctypes.byref(n))
+        return st, n.value
 
     def stats(self) -> dict:
         s = BatchStats()

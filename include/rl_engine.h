@@ -185,6 +185,46 @@ int  rl_debug_fetch(rl_engine* e, const char* what, void* out, size_t bytes);
 const char* rl_strerror(int status);
 int  rl_abi_version(void);
 
+/* ---- state export / import in the Redis keyspace layout ----
+ * The reference keeps all limiter state in Redis; these two calls move the engine's
+ * state in and out in that same layout (checkpoint / migration / hybrid deploys).
+ * One entry per live Redis key:
+ *   RL_STATE_SW_BUCKET  "rl:<key>:<window_start>" counter
+ *                       (SlidingWindowRateLimiter.java:185-188; INCR + PEXPIRE w,
+ *                        RedisRateLimitStorage.java:38-49)
+ *   RL_STATE_TB_BUCKET  "tb:<key>" hash {tokens, last_refill}
+ *                       (TokenBucketRateLimiter.java:46-48,63-64; HMSET + PEXPIRE 2w)
+ * expire_at_ms is the PEXPIRE deadline: the key is gone once now > expire_at_ms
+ * (SW: last INCR + w; TB: last_refill + 2w). */
+#define RL_STATE_SW_BUCKET 0
+#define RL_STATE_TB_BUCKET 1
+typedef struct rl_state_entry {
+    uint64_t key_hash;
+    uint16_t limiter;
+    uint8_t  kind;              /* RL_STATE_*                                          */
+    uint8_t  reserved[5];
+    int64_t  window_start_ms;   /* SW: bucket start W (a multiple of w); TB: 0         */
+    int64_t  count;             /* SW: counter value (>= 1); TB: 0                     */
+    double   tokens;            /* TB: balance, the exact fp64 the Lua script stored   */
+    int64_t  last_refill_ms;    /* TB: last_refill; SW: 0                              */
+    int64_t  expire_at_ms;      /* PEXPIRE deadline                                    */
+} rl_state_entry;               /* 56 bytes */
+
+/* Every key live at now_ns (floorDiv to ms, as the batch calls), sorted by
+ * (limiter, key_hash, window_start_ms). *n_out = number of live entries; when it
+ * exceeds cap nothing is written and RL_E_TOO_LARGE is returned (retry with a larger
+ * buffer). `out` is a host buffer. Only this engine's shard is exported. */
+int  rl_export_state(rl_engine* e, int64_t now_ns, rl_state_entry* out, size_t cap,
+                     size_t* n_out);
+/* Load entries (host buffer) into the state table, replacing the state of every key
+ * they name. A key's SW buckets are its newest bucket W and, if present, W - w (older
+ * ones can never be read again and are dropped). Entries owned by another shard are
+ * skipped; *n_imported (nullable) = entries taken. RL_E_INVALID_ARG: unknown limiter,
+ * kind not matching the limiter's algorithm, or a deadline the reference could not
+ * have set (TB: expire_at != last_refill + 2w; SW: outside [W + w, W + 2w)).
+ * RL_E_CAPACITY: a region had no free slot (the other keys are imported). */
+int  rl_import_state(rl_engine* e, const rl_state_entry* in, size_t n, size_t* n_imported);
+
 /* ---- multi-GPU routing helpers (device buffers, engine stream) ------------
  * owner(key_hash) is the shard that holds the key's state. rl_route_partition
  * stably partitions a batch by owner: perm[j] = source index of the j-th request

@@ -187,6 +187,36 @@ class PyOracle:
             t = x if x < capacity else capacity
         return java_d2l(t), t
 
+    # ---- state export / import in the Redis layout (rl_export_state / rl_import_state) ----
+    def keyspace(self, now_ms):
+        """Every key live at now_ms (RedisRateLimitStorage.java:52-59 expiry) as tuples
+        (limiter, key_hash, kind, window_start, count, tokens, last_refill, expire_at), sorted
+        like rl_export_state. SW keys "rl:<key>:<W>" (SlidingWindowRateLimiter.java:185-188),
+        TB hashes "tb:<key>" (TokenBucketRateLimiter.java:46-48,63-64)."""
+        out = []
+        for k in list(self.redis.kv):
+            if not self.redis._alive(k, now_ms):
+                continue
+            lid, rest = k.split("|", 1)
+            if rest.startswith("rl:"):
+                _, key, w0 = rest.split(":")
+                out.append((int(lid), int(key), 0, int(w0), int(self.redis.kv[k]), 0.0, 0,
+                            self.redis.exp[k]))
+            else:
+                h = self.redis.kv[k]
+                out.append((int(lid), int(rest[3:]), 1, 0, 0, h["tokens"], int(h["last_refill"]),
+                            self.redis.exp[k]))
+        out.sort(key=lambda x: (x[0], x[1], x[3]))
+        return out
+
+    def load_keyspace(self, entries):
+        """Inverse of keyspace(): SET/HMSET each entry with its PEXPIRE deadline."""
+        for lid, key, kind, w0, count, tokens, last, exp in entries:
+            k = f"{lid}|rl:{key}:{w0}" if kind == 0 else f"{lid}|tb:{key}"
+            self.redis.kv[k] = int(count) if kind == 0 else {"tokens": float(tokens),
+                                                              "last_refill": float(last)}
+            self.redis.exp[k] = int(exp)
+
     def run(self, keys, permits, now_ns, limiter=None, ops=None):
         """Replay requests in arrival order; returns (allowed, remaining, tokens_after)."""
         n = len(keys)
