@@ -1057,3 +1057,30 @@ extern "C" int rl_import_state(rl_engine* e, const rl_state_entry* in, size_t n,
     if (n_imported) *n_imported = taken;
     return fail ? RL_E_CAPACITY : RL_OK;
 }
+
+extern "C" int rl_sweep_expired(rl_engine* e, int64_t now_ns, uint64_t* reclaimed) {
+    if (!e) return RL_E_INVALID_ARG;
+    if (reclaimed) *reclaimed = 0;
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    const int64_t now = floor_div_ms(now_ns);
+    uint32_t* d_count = nullptr;
+    if (dalloc(&d_count, e->lims.size() + 1) != RL_OK) return RL_E_NOMEM;
+    std::vector<uint32_t> h(e->lims.size() + 1, 0);
+    int rc = RL_OK;
+    if (hipMemsetAsync(d_count, 0, h.size() * sizeof(uint32_t), e->stream) != hipSuccess) rc = RL_E_DEVICE;
+    for (size_t li = 0; rc == RL_OK && li < e->lims.size(); ++li) {
+        HostLimiter& hl = e->lims[li];
+        if (launch_sweep((Slot*)hl.table, hl.table_bytes / sizeof(Slot), hl.dev, now, d_count + li,
+                         e->stream) != hipSuccess)
+            rc = RL_E_DEVICE;
+    }
+    if (rc == RL_OK && (hipMemcpyAsync(h.data(), d_count, h.size() * sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+                        hipStreamSynchronize(e->stream) != hipSuccess))
+        rc = RL_E_DEVICE;
+    dfree(d_count);
+    if (rc == RL_OK && reclaimed)
+        for (uint32_t c : h) *reclaimed += c;
+    return rc;
+}

@@ -1964,6 +1964,29 @@ __global__ __launch_bounds__(64) void k_import(ImportArgs a) {
     for (uint32_t k = lane; k < kRegionSlots; k += 64) tab[k] = S[k];
 }
 
+// TTL sweep: one thread per slot; a slot none of whose buckets is live at `now` is zeroed
+// (the criterion the region load applies, slot_live). One counter atomic per wave.
+__global__ __launch_bounds__(256) void k_sweep(Slot* __restrict__ tab, uint64_t n_slots,
+                                               DevLimiter L, int64_t now, uint32_t* count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool dead = false;
+    if (i < n_slots) {
+        const Slot v = tab[i];
+        dead = (v.tag | v.a | v.b | v.c) != 0 && !slot_live(L, v, now);
+        if (dead) tab[i] = Slot{0, 0, 0, 0};
+    }
+    const uint64_t m = __ballot(dead);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (uint32_t)__popcll(m));
+}
+
+hipError_t launch_sweep(Slot* table, uint64_t n_slots, const DevLimiter& L, int64_t now_ms,
+                        uint32_t* count, hipStream_t s) {
+    const uint64_t blocks = (n_slots + 255) / 256;
+    hipLaunchKernelGGL(k_sweep, dim3((uint32_t)blocks), dim3(256), 0, s, table, n_slots, L, now_ms,
+                       count);
+    return hipGetLastError();
+}
+
 hipError_t launch_export(const Slot* table, uint64_t n_slots, const DevLimiter& L, uint16_t lim,
                          int64_t now_ms, StateRec* out, uint32_t cap, uint32_t* count,
                          hipStream_t s) {

@@ -185,6 +185,8 @@ hipError_t launch_export(const Slot* table, uint64_t n_slots, const DevLimiter& 
                          int64_t now_ms, StateRec* out, uint32_t cap, uint32_t* count,
                          hipStream_t s);
 hipError_t launch_import(const ImportArgs& a, hipStream_t s);
+hipError_t launch_sweep(Slot* table, uint64_t n_slots, const DevLimiter& L, int64_t now_ms,
+                        uint32_t* count, hipStream_t s);
 
 hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s);
 hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s);

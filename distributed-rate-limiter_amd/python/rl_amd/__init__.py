@@ -42,6 +42,7 @@ EXPORTS = [
     "rl_route_pack", "rl_route_fold", "rl_route_unpack", "rl_debug_fetch",
     "rl_route_pack_wire", "rl_route_unwire", "rl_result_width", "rl_route_fold_packed",
     "rl_route_unpack_packed", "rl_export_state", "rl_import_state",
+    "rl_sweep_expired",
 ]
 STATE_SW_BUCKET, STATE_TB_BUCKET = 0, 1
 # rl_state_entry (include/rl_engine.h): one live Redis key ("rl:<key>:<W>" / "tb:<key>")
@@ -145,6 +146,7 @@ def lib():
     L.rl_synth_trace_device.argtypes = [vp, ctypes.POINTER(TraceSpec), sz, vp, vp, vp, vp, vp]
     L.rl_export_state.argtypes = [vp, i64, vp, sz, ctypes.POINTER(sz)]
     L.rl_import_state.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    L.rl_sweep_expired.argtypes = [vp, i64, ctypes.POINTER(ctypes.c_uint64)]
     _lib = L
     return L
 
@@ -299,6 +301,14 @@ class Engine:
         st = self._L.rl_import_state(self._h, _p(entries) if entries.shape[0] else None,
                                      entries.shape[0], ctypes.byref(n))
         return st, n.value
+
+    def sweep_expired(self, now_ns) -> int:
+        """Free every slot with no bucket live at now_ns (rl_sweep_expired); returns the count."""
+        n = ctypes.c_uint64(0)
+        st = self._L.rl_sweep_expired(self._h, int(now_ns), ctypes.byref(n))
+        if st != RL_OK:
+            raise RlError(st, "rl_sweep_expired")
+        return n.value
 
     def stats(self) -> dict:
         s = BatchStats()

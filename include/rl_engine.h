@@ -225,6 +225,13 @@ int  rl_export_state(rl_engine* e, int64_t now_ns, rl_state_entry* out, size_t c
  * RL_E_CAPACITY: a region had no free slot (the other keys are imported). */
 int  rl_import_state(rl_engine* e, const rl_state_entry* in, size_t n, size_t* n_imported);
 
+/* Background TTL sweep (Redis active expiry of the PEXPIRE deadlines set at
+ * RedisRateLimitStorage.java:41-44 and Lua :64): frees every slot none of whose buckets is live at
+ * now_ns, so table memory tracks live keys even for regions no batch touches. (Batches already
+ * drop dead slots of the regions they load.) now_ns must not exceed the now of any later request,
+ * as with Redis's own clock. *reclaimed (nullable) = slots freed. */
+int  rl_sweep_expired(rl_engine* e, int64_t now_ns, uint64_t* reclaimed);
+
 /* ---- multi-GPU routing helpers (device buffers, engine stream) ------------
  * owner(key_hash) is the shard that holds the key's state. rl_route_partition
  * stably partitions a batch by owner: perm[j] = source index of the j-th request

@@ -165,3 +165,22 @@ def test_sharded_import_takes_only_owned_keys():
         got += as_tuples(es.export_state((T0 + 2000) * NS))
     got.sort(key=lambda x: (x[0], x[1], x[3]))
     assert_keyspace(got, as_tuples(dump))
+
+
+def test_ttl_sweep_frees_exactly_the_dead_slots():
+    e, o = make()
+    run_both(e, o, trace(7, 20000, T0, T0 + 3000))
+    now_ms = T0 + 3400
+    before = e.export_state(now_ms * NS)
+    e.sweep_expired(now_ms * NS)
+    assert e.sweep_expired(now_ms * NS) == 0                 # idempotent
+    after = e.export_state(now_ms * NS)
+    assert_keyspace(as_tuples(after), as_tuples(before))     # live state untouched
+    assert_keyspace(as_tuples(after), o.keyspace(now_ms))
+    live_keys = len({(int(x["limiter"]), int(x["key_hash"])) for x in after})
+    assert live_keys > 100
+    # far in the future every remaining slot is dead: exactly the live keys are freed
+    assert e.sweep_expired((now_ms + 10_000) * NS) == live_keys
+    assert e.export_state(now_ms * NS).shape[0] == 0
+    # a swept table keeps deciding like the oracle
+    run_both(e, o, trace(8, 20000, now_ms + 10_000, now_ms + 12_000))
