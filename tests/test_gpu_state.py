@@ -184,3 +184,24 @@ def test_ttl_sweep_frees_exactly_the_dead_slots():
     assert e.export_state(now_ms * NS).shape[0] == 0
     # a swept table keeps deciding like the oracle
     run_both(e, o, trace(8, 20000, now_ms + 10_000, now_ms + 12_000))
+
+
+@pytest.mark.parametrize("algo", [rl_amd.SW, rl_amd.TB])
+def test_export_after_hot_regions(algo):
+    """Hot keys are applied by the hot-region chain (k_hot_summ / hot_chain / k_hot_fill);
+    the state it writes back must export exactly like the oracle's keyspace."""
+    from test_gpu_hot import hot_trace
+    lims = [(algo, 50, 1000, 10.0 if algo == rl_amd.TB else 0.0)]
+    e, o = make(lims)
+    e.tune("hot_threshold", 256)
+    tr = hot_trace(11, 60000, 2000, 0.4, [0], 4000, hot_keys=3, ops=0.002)
+    for sl in (slice(0, 30000), slice(30000, 60000)):
+        part = tuple(x[sl] for x in tr)
+        a, r, t, st = e.execute(*part)
+        wa, wr, wt = o.run(*part)
+        assert st == rl_amd.RL_OK
+        np.testing.assert_array_equal(a, np.asarray(wa, np.uint8))
+        np.testing.assert_array_equal(r, np.asarray(wr, np.int64))
+    end_ms = int(tr[2][-1]) // NS
+    for lag in (0, 600):
+        assert_keyspace(as_tuples(e.export_state((end_ms + lag) * NS)), o.keyspace(end_ms + lag))
