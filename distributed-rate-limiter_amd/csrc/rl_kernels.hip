@@ -95,6 +95,11 @@ constexpr bool kNtScRec = true;
 constexpr bool kNtScRec = false;
 #endif
 constexpr bool kNtScPos = !RL_TEMPORAL;
+#ifdef RL_NT_UPSWEEP
+constexpr bool kNtUp = true;
+#else
+constexpr bool kNtUp = false;
+#endif
 template <bool NT, class Rec>
 __device__ inline Rec ld_rec(const Rec* p) {
     if constexpr (NT && sizeof(Rec) == 16) {
@@ -156,7 +161,7 @@ __device__ inline uint32_t bin_of(const PartArgs& a, uint32_t i, const LimLds& L
     uint64_t h;
     uint32_t lim;
     if constexpr (RAW) {
-        h = mix64(a.key[i]);
+        h = mix64(ld<kNtUp>(a.key + i));
         lim = a.limiter ? a.limiter[i] : 0u;
         if (lim >= a.n_lim) lim = 0;  // invalid: routed to limiter 0's region, rejected there
     } else {
@@ -281,7 +286,10 @@ struct ScatterIn<Codec, false> {
     }
 };
 
-constexpr int kScatterDepth = 8;        // rounds of inputs in flight (divides kTileItems)
+#ifndef RL_SCATTER_DEPTH
+#define RL_SCATTER_DEPTH 8
+#endif
+constexpr int kScatterDepth = RL_SCATTER_DEPTH;   // rounds of inputs in flight (divides kTileItems)
 
 template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
