@@ -151,7 +151,20 @@ __device__ inline void load_lim_lds(LimLds& L, const PartArgs& a) {
 
 // Tile processed by this workgroup at iteration `it` of a persistent grid: the
 // workgroups of one XCD (blocks b, b+8, ...) take consecutive tiles.
-__device__ inline uint32_t tile_at(uint32_t it) {
+// RL_TILE_ORDER 1 (A/B knob): XCD x instead owns the contiguous chunk [x*T/8, (x+1)*T/8) and
+// its workgroups walk it 32 tiles at a time, so a bin's record run is split between XCDs 8 times
+// in total rather than once per 256 tiles. Returns >= n_tiles when this workgroup is done.
+#ifndef RL_TILE_ORDER
+#define RL_TILE_ORDER 0
+#endif
+__device__ inline uint32_t tile_at(uint32_t it, uint32_t n_tiles) {
+    if constexpr (RL_TILE_ORDER == 1) {
+        if (gridDim.x % 8 == 0) {
+            const uint32_t per = gridDim.x / 8, chunk = (n_tiles + 7) / 8;
+            const uint32_t k = it * per + blockIdx.x / 8;
+            return k < chunk ? (blockIdx.x % 8) * chunk + k : n_tiles;
+        }
+    }
     return it * gridDim.x + xcd_remap(blockIdx.x, gridDim.x);
 }
 
@@ -192,7 +205,7 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
     }
     const uint32_t mask = bins - 1;
     for (uint32_t it = 0;; ++it) {
-        const uint32_t tile = tile_at(it);
+        const uint32_t tile = tile_at(it, a.n_tiles);
         if (tile >= a.n_tiles) break;
         for (uint32_t b = t; b < bins; b += kTileThreads) hist[b] = 0;
         __syncthreads();
@@ -307,7 +320,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     uint64_t mn = ~0ULL, mx = 0;
     bool overflow = false;
     for (uint32_t it = 0;; ++it) {
-        const uint32_t tile = tile_at(it);
+        const uint32_t tile = tile_at(it, a.n_tiles);
         if (tile >= a.n_tiles) break;
         const uint32_t tile0 = tile * (uint32_t)kTile;
         __syncthreads();     // previous tile's LDS users are done
@@ -1619,7 +1632,7 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
   constexpr int NB = kTileItems / B;
   const bool simple = pos1 || a.tokens_out || (a.ablate & kAblNoGather);
   for (uint32_t it = 0;; ++it) {
-    const uint32_t tile = tile_at(it);
+    const uint32_t tile = tile_at(it, a.n_tiles);
     if (tile >= a.n_tiles) break;
     const uint32_t tbase = tile * (uint32_t)kTile + t;
     if (!simple && tile * (uint64_t)kTile + kTile <= a.n) {
