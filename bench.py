@@ -77,8 +77,22 @@ CONFIGS = {
 }
 
 # algorithmic bytes per request / per distinct key
-REQ_BYTES = 22 + 9             # key 8 + now 8 + permits 4 + limiter 2 in; allowed 1 + remaining 8 out
+REQ_IN = 8 + 8 + 4             # key 8 + now 8 + permits 4 (+ limiter 2 when there are several)
+REQ_OUT = 1 + 8                # allowed 1 + remaining 8
 KEY_BYTES = 32 + 32            # state slot read + written
+
+# Bytes each pipeline kernel must move as designed (its own I/O, per request), for the
+# per-kernel bandwidth fractions; the headline roofline is the whole step's ALGORITHMIC
+# bytes over the whole step's time.
+def kernel_io_bytes(name, n, u, n_lim, res_bytes):
+    lim = 2 if n_lim > 1 else 0
+    return {
+        "upsweep0": n * (8 + lim),
+        "scatter0": n * (REQ_IN + lim + 16 + 4),          # request in; record 16 + position 4 out
+        "upsweep1": n * 16, "scatter1": n * (16 + 16 + 4),
+        "region": n * (16 + res_bytes) + u * KEY_BYTES,   # records in, packed results out, slots
+        "unpermute": n * (4 + res_bytes + REQ_OUT),        # positions + gathered results in, decisions out
+    }.get(name)
 
 
 def dist_env():
@@ -99,6 +113,48 @@ def load_pmc(config_name, kernel):
         return None if k is None else float(k["hbm_bytes_per_launch"])
     except Exception:
         return None
+
+
+def config1_line(dev):
+    """BASELINE configs[0] (RateLimiterBenchmark.java:48-71): the single-key SW 100000/min
+    stream of 100,000 tryAcquire("user123"). The Java + Redis reference cannot run here; its
+    published 80,192 req/s (README.md:174-181) is context. Times the C oracle (1 thread, the
+    CPU port) and the engine on the same stream as one HBM-resident batch."""
+    from oracle.coracle import COracle
+    n = 100_000
+    t0 = (1_700_000_000_000 // 60000) * 60000 + 5000
+    keys = np.full(n, rl_amd.key_hash("user123"), np.uint64)
+    now = (t0 * NS + np.arange(n, dtype=np.int64) * 12_500).astype(np.int64)
+    permits = np.ones(n, np.int32)
+    lim = [(rl_amd.SW, 100_000, 60_000, 0.0)]
+    o = COracle(lim)
+    c0 = time.perf_counter()
+    oa, orem, _, _ = o.run(keys, permits, now, want_tokens=False)
+    cpu_s = time.perf_counter() - c0
+    o.close()
+    d = [torch.from_numpy(x).to(dev) for x in (keys.view(np.int64), permits, now)]
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    r = torch.empty(n, dtype=torch.int64, device=dev)
+    best = None
+    for rep in range(3):                       # a fresh engine (empty state) per repetition
+        e = rl_amd.Engine(device=dev.index or 0, max_batch=n, capacity=1 << 10)
+        e.add_limiter(*lim[0])
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        e.execute_device(n, *d, None, None, a, r)
+        e.sync()
+        dt = time.perf_counter() - g0
+        best = dt if best is None else min(best, dt)
+        e.close()
+    ok = bool(np.array_equal(a.cpu().numpy(), oa) and np.array_equal(r.cpu().numpy(), orem))
+    return {"workload": "RateLimiterBenchmark sliding window single key user123, max 100000/min, "
+                        "100,000 requests (RateLimiterBenchmark.java:48-71)",
+            "allowed": int(oa.sum()), "parity": "bit-exact" if ok else "MISMATCH",
+            "engine_value": n / best, "engine_ms": best * 1e3,
+            "cpu_port_value": n / cpu_s, "cpu_port_cores": 1,
+            "reference_published": 80192, "unit": "decisions/s",
+            "note": "engine = one HBM-resident batch (hot-key chain of 100k requests); the "
+                    "micro-batched host path is timed by tests/cpp/test_host_api (config1)"}
 
 
 def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remaining):
@@ -144,6 +200,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--tune", action="append", default=[],
                     help="engine knob key=value (rl_tune), e.g. bin_shift=0")
+    ap.add_argument("--stage-timing", action="store_true",
+                    help="also record hipEvents inside the timed steps (diagnostics only)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -169,8 +227,10 @@ def main():
     # weak scaling: each shard owns 1/ws of the keys but sees ws x n requests' worth of
     # key space across ranks, i.e. the same number of requests per GPU; a shard's table
     # is sized for its share of the global key population.
-    eng = rl_amd.Engine(device=local, max_batch=n * (2 if ws > 1 else 1),
-                        capacity=cfg["capacity"] * ws, stage_timing=True, shard_index=rank,
+    # an owner can receive up to ws x n requests in a skewed step (the router grows its
+    # receive buffers; the engine's scratch is allocated for what it actually receives)
+    eng = rl_amd.Engine(device=local, max_batch=n * ws,
+                        capacity=cfg["capacity"] * ws, stage_timing=False, shard_index=rank,
                         shard_count=ws)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)
@@ -211,14 +271,21 @@ def main():
             k, p, t, li = inputs[s]
             eng.execute_device(n, k, p, t, li, None, allowed, remaining)
 
+    # Warmup steps. Steps 1.. of the warmup carry hipEvents between the stages (the
+    # per-stage breakdown); the timed steps below run without them.
     keep0 = None
+    stages = {}
     for s in range(warm):
+        if s == 1:
+            eng.tune("stage_timing", 1)
         step(s)
         if s == 0:
             eng.sync()
             keep0 = (allowed.cpu().numpy(), remaining.cpu().numpy())
+    if warm > 1:
+        stages = eng.stage_times()
+    eng.tune("stage_timing", 1 if args.stage_timing else 0)
     st = eng.last_status()
-    eng.stage_times()                      # drop warmup stage samples
 
     if ws > 1:
         dist.barrier()
@@ -232,22 +299,34 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if ws > 1:
+        router.finish()                    # collective: raises on every rank on an engine error
+    if ws > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     st = eng.last_status()
     stats = eng.stats()
-    stages = eng.stage_times()
+    if args.stage_timing:
+        stages = eng.stage_times()
     ms_per_step = elapsed / steps * 1e3
     value = ws * n * steps / elapsed
 
-    kern = {k: v for k, v in stages.items() if k != "total" and v > 0}
-    dom = max(kern, key=kern.get)
+    kern = {k: v for k, v in stages.items() if k not in ("total", "region_offsets") and v > 0}
     U = stats["distinct_keys"]
-    algo_bytes = n * REQ_BYTES + U * KEY_BYTES
-    achieved = algo_bytes / (kern[dom] * 1e-3) / 1e9
-    step_gbs = algo_bytes * ws / (elapsed / steps) / 1e9
-    traffic = load_pmc(args.config, dom)
+    n_lim = len(cfg["limiters"])
+    req_bytes = REQ_IN + (2 if n_lim > 1 else 0) + REQ_OUT
+    algo_bytes = n * req_bytes + U * KEY_BYTES            # per GPU per step
+    step_s = elapsed / steps
+    achieved = algo_bytes * ws / step_s / 1e9             # whole node
+    peak = HBM_PEAK_GBS * ws
+    traffic = load_pmc(args.config, "step")
+    res_b = eng.result_width()
+    kernels = {}
+    for k, ms in kern.items():
+        io = kernel_io_bytes(k, n, U, n_lim, res_b)
+        kernels[k] = {"ms": round(ms, 4), "io_bytes": io,
+                      "io_frac": None if io is None else round(io / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    dom = max(kern, key=kern.get) if kern else None
 
     out = {
         "metric": "rate-limit decisions/sec (whole node)",
@@ -265,11 +344,14 @@ def main():
         "config": {"workload": f"{args.config}: {cfg['desc']}", "requests_per_gpu_per_step": n,
                    "n_keys": cfg["n_keys"] * ws, "n_limiters": n_lim, "parallelism": f"key-hash shards x{ws}"
                    + (" + RCCL all-to-all routing" if ws > 1 else "")},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom,
-                     "kernel_ms": kern[dom],
-                     "algorithmic_bytes_per_launch": algo_bytes,
-                     "step_frac": step_gbs / (HBM_PEAK_GBS * ws)},
+        # Headline: the whole step's ALGORITHMIC bytes (N x (in + out) + U x
+        # (slot read + write)) over the whole step's wall time, against 8 TB/s per GPU. The
+        # step is one launch sequence of the pipeline kernels; `kernels` breaks it down.
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": traffic, "kernel": "pipeline (one step)",
+                     "algorithmic_bytes_per_step": algo_bytes,
+                     "bytes_per_request": req_bytes, "distinct_keys_per_step": U,
+                     "dominant_kernel": dom, "kernels": kernels},
         "stage_ms": {k: round(v, 4) for k, v in stages.items()},
         "batch_stats": {k: stats[k] for k in ("allowed", "distinct_keys", "invalid",
                                               "capacity_errors", "regions_touched")},
@@ -281,6 +363,7 @@ def main():
         out["cpu_baseline"] = cb
         out["parity"] = f"{'bit-exact' if parity else 'MISMATCH'} vs oracle on the first {m} " \
                         f"requests of batch 0"
+        out["config1"] = config1_line(dev)
     else:
         out["cpu_baseline"] = None
     if rank == 0:

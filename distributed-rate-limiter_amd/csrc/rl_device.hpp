@@ -193,6 +193,17 @@ constexpr int64_t kResBias = 3;
 __device__ inline uint64_t pack_result(bool allowed, int64_t remaining) {
     return ((uint64_t)(remaining + kResBias) << 1) | (allowed ? 1u : 0u);
 }
+// A token-bucket balance goes below -3 only after time regression (elapsed < 0 is not
+// clamped, Lua :56-58), and its reply integer can be any negative value. `remaining = -3`
+// is never allowed, so the packed code 1 (= pack_result(true, -3)) is free: it marks a
+// remaining outside the width's range, kept exactly in an int64 side array (`ext`) at the
+// same position and restored by the unpermute.
+constexpr uint64_t kResEscape = 1;
+template <class Res>
+__device__ inline bool res_fits(int64_t remaining) {
+    constexpr int64_t hi = (int64_t)((uint64_t)(Res)~(Res)0 >> 1) - kResBias;
+    return remaining >= -kResBias && remaining <= hi;
+}
 __host__ __device__ inline int res_bytes_for(int64_t max_permits, bool wide) {
     if (wide) return 8;
     if ((max_permits + kResBias) * 2 + 1 < 256) return 1;
@@ -363,18 +374,41 @@ __device__ inline Outcome sw_step_g(const DevLimiter& L, uint32_t op, int32_t pe
         return o;
     }
     // incrementAndExpire(currentKey, w) (:114-116, RedisRateLimitStorage.java:38-49)
+    uint32_t new_count;
     if (s.b1_start == curr_start) {
         const bool alive = s.b1_cnt != 0 && !(now > s.b1_start + s.b1_off + w);
         s.b1_cnt = alive ? s.b1_cnt + 1 : 1;
-    } else {                                         // a newer window (now is per-key monotone)
+        s.b1_off = (int32_t)(now - curr_start);
+        new_count = s.b1_cnt;
+    } else if (curr_start > s.b1_start || (s.b1_cnt == 0 && s.b0_cnt == 0)) {   // a newer window
         if (s.b1_start == curr_start - w) { s.b0_cnt = s.b1_cnt; s.b0_off = s.b1_off; }
         else { s.b0_cnt = 0; s.b0_off = 0; }
         s.b1_start = curr_start;
         s.b1_cnt = 1;
+        s.b1_off = (int32_t)(now - curr_start);
+        new_count = 1;
+    } else if (curr_start == s.b1_start - w) {
+        // time regression into the previous window (e.g. front-ends with skewed clocks):
+        // Redis keeps every window's key, so the INCR lands on bucket b0 and the newer bucket
+        // is untouched. PEXPIRE sets its deadline from this request's now.
+        const int64_t b0_start = s.b1_start - w;
+        const bool alive = s.b0_cnt != 0 && !(now > b0_start + s.b0_off + w);
+        s.b0_cnt = alive ? s.b0_cnt + 1 : 1;
+        s.b0_off = (int32_t)(now - b0_start);
+        new_count = s.b0_cnt;
+    } else {
+        // regression past both tracked buckets: the bucket it increments (and the one before
+        // it) are older than the key's newest two and are not kept; they read as absent, so
+        // the INCR yields 1 (documented divergence). The newer buckets are
+        // never rolled back.
+        o.mutate = false;
+        o.allowed = 1 <= L.max_permits;
+        const int64_t r = L.max_permits - 1;              // estimate after: 0 * pw + 1
+        o.remaining = r > 0 ? r : 0;
+        return o;
     }
-    s.b1_off = (int32_t)(now - curr_start);
     o.mutate = true;
-    o.allowed = (int64_t)s.b1_cnt <= L.max_permits;  // :123
+    o.allowed = (int64_t)new_count <= L.max_permits;  // :123
     const int64_t est2 = sw_estimate(s, geo, now, w);  // remaining after the request (A4)
     const int64_t r = L.max_permits - est2;
     o.remaining = r > 0 ? r : 0;

@@ -69,6 +69,7 @@ struct rl_engine {
     uint32_t* pos0 = nullptr;
     uint32_t* pos1 = nullptr;
     void* res = nullptr;
+    int64_t* ext = nullptr;                 // escaped remainders (kResEscape), like res
     double* tok = nullptr;
     uint32_t* counts = nullptr;             // [bins][tiles]
     size_t counts_cap = 0;
@@ -130,6 +131,12 @@ struct rl_engine {
             return RL_E_DEVICE;                                        \
         }                                                              \
     } while (0)
+
+static void ensure_events(rl_engine* e) {
+    if (e->ev[0][0]) return;
+    for (int r = 0; r < kEvRing; ++r)
+        for (int i = 0; i < kMarks; ++i) (void)hipEventCreate(&e->ev[r][i]);
+}
 
 static void dfree(void*& p) {
     if (p) (void)hipFree(p);
@@ -201,9 +208,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
         return RL_E_DEVICE;
     }
     e->timing = (o.flags & RL_OPT_STAGE_TIMING) != 0;
-    if (e->timing)
-        for (int r = 0; r < kEvRing; ++r)
-            for (int i = 0; i < kMarks; ++i) (void)hipEventCreate(&e->ev[r][i]);
+    if (e->timing) ensure_events(e);
     int rc = dalloc(&e->d_ctl, 1);
     if (rc == RL_OK && hipHostMalloc((void**)&e->h_ctl, sizeof(BatchCtl)) != hipSuccess) rc = RL_E_NOMEM;
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
@@ -223,6 +228,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     for (auto& l : e->lims) dfree(l.table);
     dfree(e->d_lims); dfree(e->d_region_lim);
     dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
+    dfree(e->ext);
     dfree(e->counts); dfree(e->bin_total); dfree(e->bin_base);
     dfree(e->region_count); dfree(e->region_start);
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
@@ -317,12 +323,14 @@ static int ensure_scratch(rl_engine* e, size_t n, bool wide, uint32_t bins, uint
         const size_t rb = wide ? sizeof(RecW) : sizeof(RecC);
         const size_t padn = cap + kTileThreads;   // kernels write inactive lanes past n
         dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
+        dfree(e->ext);
         int rc = dalloc(&e->rec0, padn * rb);
         if (rc == RL_OK) rc = dalloc(&e->rec1, padn * rb);
         if (rc == RL_OK) rc = dalloc(&e->pos0, padn);
         if (rc == RL_OK) rc = dalloc(&e->pos1, padn);
         if (rc == RL_OK) rc = dalloc(&e->res, padn * sizeof(uint64_t));
         if (rc == RL_OK) rc = dalloc(&e->tok, padn);
+        if (rc == RL_OK) rc = dalloc(&e->ext, padn);
         if (rc != RL_OK) { e->cap_n = 0; return rc; }
         e->cap_n = cap;
         e->cap_wide = wide;
@@ -484,7 +492,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     RegionArgs ra{};
     ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.rend = rend;
     ra.region_lim = e->d_region_lim;
-    ra.lims = e->d_lims; ra.res = e->res; ra.tok = tokens_after ? e->tok : nullptr;
+    ra.lims = e->d_lims; ra.res = e->res; ra.ext = e->ext; ra.tok = tokens_after ? e->tok : nullptr;
     ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
     if (e->debug_regions) {
@@ -517,6 +525,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
     ua.mid = e->rec0;                                    // pass-0 records are dead by now
     ua.tok = tokens_after ? e->tok : nullptr;
+    ua.ext = e->ext; ua.ctl = e->d_ctl;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
     ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate; ua.per_cu = e->un_per_cu;
     HIP_OK(launch_unpermute(ua, res_bytes, s));
@@ -701,6 +710,12 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "scatter_per_cu") == 0) { e->sc_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "unpermute_per_cu") == 0) { e->un_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "debug_regions") == 0) { e->debug_regions = value != 0; return RL_OK; }
+    if (std::strcmp(key, "stage_timing") == 0) {     // hipEvents around every stage on/off
+        if (value) ensure_events(e);
+        e->timing = value != 0;
+        e->ring_used = 0;
+        return RL_OK;
+    }
     if (std::strcmp(key, "hot_threshold") == 0) {      // records per region; 0 = no hot path
         if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
         e->hot_threshold = (uint32_t)value;
@@ -844,6 +859,74 @@ extern "C" int rl_route_unpack_packed(rl_engine* e, size_t n, const uint32_t* pe
     (void)hipSetDevice(e->device);
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     HIP_OK(launch_route_unpack_w((uint32_t)n, perm, packed, width, allowed, remaining, s));
+    return RL_OK;
+}
+
+extern "C" uint64_t rl_route_return_bytes(uint32_t n_seg, const uint64_t* seg_counts, int width,
+                                          uint32_t exc_cap) {
+    if (!seg_counts || n_seg == 0 || n_seg > (uint32_t)kMaxShards) return 0;
+    if (width != 1 && width != 2 && width != 4 && width != 8) return 0;
+    return ret_layout(seg_counts, n_seg, width, exc_cap, nullptr, nullptr);
+}
+
+extern "C" int rl_route_fold_return(rl_engine* e, size_t m, const uint8_t* allowed,
+                                    const int64_t* remaining, void* out, int width, uint32_t n_seg,
+                                    const uint64_t* seg_counts, uint32_t exc_cap, void* stream) {
+    if (!e || !out || !seg_counts || (m && (!allowed || !remaining))) return RL_E_INVALID_ARG;
+    if (width != 1 && width != 2 && width != 4 && width != 8) return RL_E_INVALID_ARG;
+    if (n_seg == 0 || n_seg > (uint32_t)kMaxShards || m > 0xFFFFFFF0ULL) return RL_E_INVALID_ARG;
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < n_seg; ++i) tot += seg_counts[i];
+    if (tot != m) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_fold_ret((uint32_t)m, allowed, remaining, out, width, n_seg, seg_counts,
+                                 exc_cap, s));
+    return RL_OK;
+}
+
+extern "C" int rl_route_unpack_return(rl_engine* e, size_t n, const uint32_t* perm, const void* in,
+                                      int width, uint32_t n_seg, const uint64_t* seg_counts,
+                                      uint32_t exc_cap, uint8_t* allowed, int64_t* remaining,
+                                      uint32_t* lost, void* stream) {
+    if (!e || !seg_counts || !lost || (n && (!perm || !in || !allowed || !remaining)))
+        return RL_E_INVALID_ARG;
+    if (width != 1 && width != 2 && width != 4 && width != 8) return RL_E_INVALID_ARG;
+    if (n_seg == 0 || n_seg > (uint32_t)kMaxShards || n > 0xFFFFFFF0ULL) return RL_E_INVALID_ARG;
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < n_seg; ++i) tot += seg_counts[i];
+    if (tot != n) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_unpack_ret((uint32_t)n, perm, in, width, n_seg, seg_counts, exc_cap, allowed,
+                                   remaining, lost, s));
+    return RL_OK;
+}
+
+extern "C" int rl_route_partition_device(rl_engine* e, size_t n, const uint64_t* key_hash,
+                                         uint32_t shard_count, uint32_t* perm, int64_t* counts_dev,
+                                         size_t counts_stride, void* stream) {
+    if (!e || !key_hash || !perm || !counts_dev || counts_stride == 0) return RL_E_INVALID_ARG;
+    if (shard_count == 0 || shard_count > 64 || (shard_count & (shard_count - 1))) return RL_E_INVALID_ARG;
+    if (n > 0xFFFFFFF0ULL) return RL_E_TOO_LARGE;
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    const size_t nt = (n + kTile - 1) / kTile;
+    const size_t need = (size_t)shard_count * std::max<size_t>(nt, 1) + 64;
+    if (need > e->route_cap) {
+        dfree(e->route_scratch);
+        if (dalloc(&e->route_scratch, need) != RL_OK) return RL_E_NOMEM;
+        e->route_cap = need;
+    }
+    if (!e->route_counts && dalloc(&e->route_counts, 64) != RL_OK) return RL_E_NOMEM;
+    if (n == 0) {
+        HIP_OK(hipMemsetAsync(e->route_counts, 0, 64 * sizeof(uint32_t), s));
+    } else {
+        HIP_OK(launch_owner_partition(key_hash, (uint32_t)n, shard_count, perm, e->route_counts,
+                                      e->route_scratch, s));
+    }
+    HIP_OK(launch_counts_to_header(e->route_counts, shard_count, counts_dev, (uint32_t)counts_stride, s));
     return RL_OK;
 }
 

@@ -57,6 +57,15 @@ __device__ inline uint64_t wave_match(uint32_t v, int nbits, bool active) {
 
 __device__ inline uint64_t ord_key(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ULL; }
 
+// Earliest / latest now_ms of the batch's valid requests. A batch with no valid request
+// has min = INT64_MIN (every stored bucket is kept when a region is loaded) and max = lo.
+__device__ inline int64_t batch_lo(const BatchCtl* c) {
+    return c->min_now_key == ~0ULL ? INT64_MIN : (int64_t)(c->min_now_key ^ 0x8000000000000000ULL);
+}
+__device__ inline int64_t batch_hi(const BatchCtl* c) {
+    return c->max_now_key == 0ULL ? batch_lo(c) : (int64_t)(c->max_now_key ^ 0x8000000000000000ULL);
+}
+
 // Streaming (non-temporal) accesses for data touched once per batch: the scatter's request
 // reads and position writes, the region kernel's record stream (one region per bin) and
 // unpermute's position reads and output writes. They keep L2 / Infinity Cache for the
@@ -200,6 +209,7 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
             c->min_now_key = ~0ULL;
             c->max_now_key = 0;
             c->span_overflow = 0;
+            c->n_esc = 0;
             c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = 0;
         }
     }
@@ -351,11 +361,17 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                     if (op > 2u) op = 0;
                     const uint64_t h = mix64(in.key);
                     rec = Codec::enc(h, now_ms, base, p, op, lim, invalid);
-                    const int64_t rel = now_ms - base;
-                    overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
-                    const uint64_t k = ord_key(now_ms);
-                    mn = k < mn ? k : mn;
-                    mx = k > mx ? k : mx;
+                    // an invalid request's now is never read: it neither widens the batch's
+                    // time range nor rejects the batch for its span
+                    if (!invalid) {
+                        const int64_t rel = now_ms - base;
+                        // only the compact record keeps now relative to base
+                        if constexpr (std::is_same<Codec, CodecC>::value)
+                            overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
+                        const uint64_t k = ord_key(now_ms);
+                        mn = k < mn ? k : mn;
+                        mx = k > mx ? k : mx;
+                    }
                     d = (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
                          >> a.digit_shift) & mask;
                 } else {
@@ -454,9 +470,25 @@ struct RegionLds<Codec, false> : RegionTable {};
 
 struct Applied {
     uint32_t j;                       // result index (padding slot for idle lanes)
-    uint64_t out;                     // packed result
+    bool alw;                         // allowed
+    int64_t rem;                      // remaining
     double tok;
 };
+
+// Result store in partition order: packed in the width Res, or the escape code plus the
+// exact value in the int64 side array when remaining is outside Res's range (a TB
+// balance below -3 after time regression; see kResEscape).
+template <class Res>
+__device__ inline void put_res(const RegionArgs& a, uint32_t j, bool alw, int64_t rem) {
+    Res* res = (Res*)a.res;
+    if (res_fits<Res>(rem)) {
+        res[j] = (Res)pack_result(alw, rem);
+    } else {
+        res[j] = (Res)kResEscape;
+        a.ext[j] = rem;
+        atomicAdd(&a.ctl->n_esc, 1u);
+    }
+}
 
 // Apply one group of up to 64 requests (lane order = arrival order; `valid` lanes only).
 template <class Codec, int ALGO, class LdsT>
@@ -470,7 +502,8 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
     r.j = valid ? j : pad;
     const Req q = Codec::dec(cur, base);
     const bool live = valid && !q.invalid;
-    r.out = pack_result(false, kRemInvalid);
+    r.alw = false;
+    r.rem = kRemInvalid;
     r.tok = __builtin_nan("");
     n_invalid += (valid && q.invalid) ? 1u : 0u;
     // ---- find or insert the key's slot (lookup phase, then claim phase)
@@ -512,7 +545,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         wave_fence();
     }
     if (failed) {
-        r.out = pack_result(false, kRemError);
+        r.rem = kRemError;
         ++n_caperr;
     }
     if (slot >= 0) atomicOr(&S.occ[slot], 2u);
@@ -587,7 +620,8 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                         sw_commit_allows(L, geo, na, nb, nc, (uint32_t)__popcll(ok), q.now_ms);
                         S.sa[slot] = na; S.sb[slot] = nb; S.sc[slot] = nc;
                     }
-                    r.out = pack_result(al.allowed, al.remaining);
+                    r.alw = al.allowed;
+                    r.rem = al.remaining;
                     r.tok = __builtin_nan("");
                     n_allowed += al.allowed ? 1u : 0u;
                     pending = false;
@@ -595,7 +629,8 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             }
         } else if (pending && lane <= fm) {
             if (lane == fm) { S.sa[slot] = o.a; S.sb[slot] = o.b; S.sc[slot] = o.c; }
-            r.out = pack_result(o.allowed, o.remaining);
+            r.alw = o.allowed;
+            r.rem = o.remaining;
             r.tok = o.tokens;
             n_allowed += o.allowed ? 1u : 0u;
             pending = false;
@@ -625,7 +660,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     const uint32_t region = bin * RPB + rb;
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
-    const int64_t batch_min = (int64_t)(a.ctl->min_now_key ^ 0x8000000000000000ULL);
+    const int64_t batch_min = batch_lo(a.ctl);
     const uint32_t pad = a.n_total + lane;          // padding slot for idle lanes
     const Rec* recs = (const Rec*)a.rec;
     Res* res = (Res*)a.res;
@@ -683,7 +718,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 // the bin is the region: every record is ours, applied straight from registers
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, idx < end, idx, base, pad,
                                                      n_allowed, n_invalid, n_caperr, n_rounds);
-                res[ap.j] = (Res)ap.out;
+                put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             } else {
                 const bool mine = idx < end &&
@@ -697,7 +732,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 count += (uint32_t)__popcll(bal);
                 wave_fence();
                 Applied ap;
-                ap.j = pad; ap.out = 0; ap.tok = 0.0;
+                ap.j = pad; ap.alw = false; ap.rem = kRemError; ap.tok = 0.0;
                 if (count >= 64) {
                     const uint32_t ri = (head + lane) % kRing;
                     ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
@@ -705,7 +740,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                     head = (head + 64) % kRing;
                     count -= 64;
                 }
-                res[ap.j] = (Res)ap.out;                 // exactly one store per slice
+                put_res<Res>(a, ap.j, ap.alw, ap.rem);   // exactly one store per slice
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
         };
@@ -730,7 +765,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
                                                      pad, n_allowed, n_invalid, n_caperr, n_rounds);
-                res[ap.j] = (Res)ap.out;
+                put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
         }
@@ -1081,8 +1116,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     const uint32_t region = f.bin;                    // bin_shift 0: bin == region
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
-    const int64_t lo = (int64_t)(a.ctl->min_now_key ^ 0x8000000000000000ULL);
-    const int64_t hi = (int64_t)(a.ctl->max_now_key ^ 0x8000000000000000ULL);
+    const int64_t lo = batch_lo(a.ctl);
+    const int64_t hi = batch_hi(a.ctl);
     const Rec* recs = (const Rec*)a.rec;
     Res* res = (Res*)a.res;
     const uint32_t pad = a.n_total + lane;
@@ -1166,11 +1201,12 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             pre = recs[min(f.start + pre_c * kHotChunk + lane, f.end - 1)];
             const Req q = Codec::dec(r, base);
             const bool hot = is_hot(q, valid);
-            uint64_t out = 0;
+            bool oa = false;
+            int64_t orem = 0;
             double tk = __builtin_nan("");
             bool pend = hot;
             if (A == kAlgoTB && hot && q.op == (uint32_t)kOpAcquire && (int64_t)q.permits > L.max_permits) {
-                out = pack_result(false, kRemUnknown);    // :110-116, no state access
+                orem = kRemUnknown;                       // :110-116, no state access
                 pend = false;
             }
             {
@@ -1178,7 +1214,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 const uint64_t m = __ballot(pend && !fast);
                 const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
                 if (pend && lane < first) {               // inside [T0, T1): denied, remaining 0
-                    out = pack_result(false, 0);
+                    orem = 0;
                     if (TOK && A == kAlgoTB) tk = tb_refill(L, q.now_ms, S.sa[hs], S.sb[hs], S.sc[hs]);
                     pend = false;
                 }
@@ -1240,7 +1276,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                             gl.prev_weight = __shfl(geo.prev_weight, (int)last, 64);
                             sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)__popcll(ok), t_last);
                             if (pend && lane <= fa) {
-                                out = pack_result(al.allowed, al.remaining);
+                                oa = al.allowed;
+                                orem = al.remaining;
                                 n_allowed += al.allowed ? 1u : 0u;
                                 pend = false;
                             }
@@ -1248,7 +1285,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         }
                     } else {
                         if (pend && lane <= fm) {
-                            out = pack_result(o.allowed, o.remaining);
+                            oa = o.allowed;
+                            orem = o.remaining;
                             tk = o.tokens;
                             n_allowed += o.allowed ? 1u : 0u;
                             pend = false;
@@ -1285,7 +1323,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 }
             }
             if (hot) {
-                res[j] = (Res)out;
+                put_res<Res>(a, j, oa, orem);
                 if (TOK) a.tok[j] = tk;
             }
             prev_detail = c;
@@ -1364,7 +1402,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds);
             if (v) {
-                res[ap.j] = (Res)ap.out;
+                put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
         };
@@ -1699,6 +1737,26 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
         }
     }
   }
+  if (a.ctl && a.ctl->n_esc != 0) {
+    // Rare (TB balances below -3 after time regression): the gather above decoded the
+    // escape code as (allowed 1, remaining -3); rewrite those results from the side array.
+    // Same tiles, same thread per element as above, so the rewrite follows the first store.
+    const Res* rf = (const Res*)a.res_final;
+    for (uint32_t it = 0;; ++it) {
+      const uint32_t tile = tile_at(it, a.n_tiles);
+      if (tile >= a.n_tiles) break;
+      for (int r = 0; r < kTileItems; ++r) {
+        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        if (i >= a.n) break;
+        uint32_t j = pos0[i];
+        if (a.pos1_final) j = a.pos1_final[j];
+        if ((uint64_t)rf[j] == kResEscape) {
+          allowed[i] = 0;
+          remaining[i] = a.ext[j];
+        }
+      }
+    }
+  }
 }
 
 // Two-pass batches: undo the high-digit pass first. mid[j] = res[pos1[j]] for j in
@@ -1957,6 +2015,139 @@ __global__ __launch_bounds__(256) void k_route_unpack_w(uint32_t n, const uint32
     remaining[i] = (int64_t)(v >> 1) - kResBias;
 }
 
+// Return trip in segments (router): the decisions for peer s travel as
+//   [ round8(count_s * W) bytes of packed results ][ exception block ]
+// where the block = {count u64, cap x (position i64, remaining i64)} lists the results
+// whose remaining is outside W's range (TB balances below -3 after time regression,
+// kResEscape). One all-to-all carries both, with byte splits the host already knows from
+// the header exchange; nothing else crosses for the rare exact values.
+struct RetLayout {
+    uint64_t off[kMaxShards];    // byte offset of segment s
+    uint32_t end[kMaxShards];    // requests [end[s-1], end[s]) belong to segment s
+    uint32_t n_seg;
+    uint32_t cap;                // exception entries per block
+};
+
+__device__ inline uint32_t seg_of(const RetLayout& L, uint32_t j) {
+    uint32_t s = 0;
+    while (s + 1 < L.n_seg && j >= L.end[s]) ++s;
+    return s;
+}
+__device__ inline uint64_t seg_block(const RetLayout& L, uint32_t s, uint32_t W) {
+    const uint32_t beg = s ? L.end[s - 1] : 0u;
+    return L.off[s] + (((uint64_t)(L.end[s] - beg) * W + 7) & ~7ULL);
+}
+
+__global__ __launch_bounds__(64) void k_ret_init(uint8_t* out, RetLayout L, uint32_t W) {
+    for (uint32_t s = threadIdx.x; s < L.n_seg; s += 64) *(uint64_t*)(out + seg_block(L, s, W)) = 0;
+}
+
+template <class W>
+__global__ __launch_bounds__(256) void k_route_fold_ret(uint32_t m, const uint8_t* __restrict__ allowed,
+                                                        const int64_t* __restrict__ remaining,
+                                                        uint8_t* __restrict__ out, RetLayout L) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t s = seg_of(L, j);
+    const uint32_t beg = s ? L.end[s - 1] : 0u;
+    const int64_t rem = remaining[j];
+    W* seg = (W*)(out + L.off[s]);
+    if (res_fits<W>(rem)) {
+        seg[j - beg] = (W)pack_result(allowed[j] & 1u, rem);
+    } else {
+        seg[j - beg] = (W)kResEscape;
+        uint64_t* blk = (uint64_t*)(out + seg_block(L, s, sizeof(W)));
+        const uint64_t k = atomicAdd((unsigned long long*)blk, 1ULL);
+        if (k < L.cap) { blk[1 + 2 * k] = j - beg; blk[2 + 2 * k] = (uint64_t)rem; }
+    }
+}
+
+template <class W>
+__global__ __launch_bounds__(256) void k_route_unpack_ret(uint32_t n, const uint32_t* __restrict__ perm,
+                                                          const uint8_t* __restrict__ in, RetLayout L,
+                                                          uint8_t* __restrict__ allowed,
+                                                          int64_t* __restrict__ remaining,
+                                                          uint32_t* __restrict__ lost) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t s = seg_of(L, j);
+    const uint32_t beg = s ? L.end[s - 1] : 0u;
+    const uint64_t v = (uint64_t)((const W*)(in + L.off[s]))[j - beg];
+    const uint32_t i = perm[j];
+    if (v != kResEscape) {
+        allowed[i] = (uint8_t)(v & 1u);
+        remaining[i] = (int64_t)(v >> 1) - kResBias;
+        return;
+    }
+    const uint64_t* blk = (const uint64_t*)(in + seg_block(L, s, sizeof(W)));
+    const uint64_t cnt = blk[0] < L.cap ? blk[0] : L.cap;
+    int64_t r = kRemError;                       // not found: the block overflowed
+    bool found = false;
+    for (uint64_t k = 0; k < cnt; ++k)
+        if (blk[1 + 2 * k] == j - beg) { r = (int64_t)blk[2 + 2 * k]; found = true; break; }
+    if (!found) atomicAdd(lost, 1u);
+    allowed[i] = 0;
+    remaining[i] = r;
+}
+
+hipError_t launch_route_fold_ret(uint32_t m, const uint8_t* allowed, const int64_t* remaining,
+                                 void* out, int width, uint32_t n_seg, const uint64_t* counts,
+                                 uint32_t cap, hipStream_t s) {
+    if (n_seg == 0 || n_seg > (uint32_t)kMaxShards) return hipErrorInvalidValue;
+    RetLayout L{};
+    ret_layout(counts, n_seg, width, cap, L.off, L.end);
+    L.n_seg = n_seg;
+    L.cap = cap;
+    hipLaunchKernelGGL(k_ret_init, dim3(1), dim3(64), 0, s, (uint8_t*)out, L, (uint32_t)width);
+    if (m == 0) return hipGetLastError();
+    const dim3 g((m + 255) / 256), b(256);
+    uint8_t* o = (uint8_t*)out;
+    switch (width) {
+    case 1: hipLaunchKernelGGL(k_route_fold_ret<uint8_t>, g, b, 0, s, m, allowed, remaining, o, L); break;
+    case 2: hipLaunchKernelGGL(k_route_fold_ret<uint16_t>, g, b, 0, s, m, allowed, remaining, o, L); break;
+    case 4: hipLaunchKernelGGL(k_route_fold_ret<uint32_t>, g, b, 0, s, m, allowed, remaining, o, L); break;
+    case 8: hipLaunchKernelGGL(k_route_fold_ret<uint64_t>, g, b, 0, s, m, allowed, remaining, o, L); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_route_unpack_ret(uint32_t n, const uint32_t* perm, const void* in, int width,
+                                   uint32_t n_seg, const uint64_t* counts, uint32_t cap,
+                                   uint8_t* allowed, int64_t* remaining, uint32_t* lost,
+                                   hipStream_t s) {
+    if (n_seg == 0 || n_seg > (uint32_t)kMaxShards) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    RetLayout L{};
+    ret_layout(counts, n_seg, width, cap, L.off, L.end);
+    L.n_seg = n_seg;
+    L.cap = cap;
+    const dim3 g((n + 255) / 256), b(256);
+    const uint8_t* x = (const uint8_t*)in;
+    switch (width) {
+    case 1: hipLaunchKernelGGL(k_route_unpack_ret<uint8_t>, g, b, 0, s, n, perm, x, L, allowed, remaining, lost); break;
+    case 2: hipLaunchKernelGGL(k_route_unpack_ret<uint16_t>, g, b, 0, s, n, perm, x, L, allowed, remaining, lost); break;
+    case 4: hipLaunchKernelGGL(k_route_unpack_ret<uint32_t>, g, b, 0, s, n, perm, x, L, allowed, remaining, lost); break;
+    case 8: hipLaunchKernelGGL(k_route_unpack_ret<uint64_t>, g, b, 0, s, n, perm, x, L, allowed, remaining, lost); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// Owner partition with the per-owner counts left on the device as int64 (column 0 of the
+// router's G x 3 header, `stride` int64 apart): no host round-trip before the header
+// exchange.
+__global__ void k_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride) {
+    const uint32_t t = threadIdx.x;
+    if (t < g) hdr[(size_t)t * stride] = counts[t];
+}
+
+hipError_t launch_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride,
+                                   hipStream_t s) {
+    hipLaunchKernelGGL(k_counts_to_header, dim3(1), dim3(64), 0, s, counts, g, hdr, stride);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ state export / import
 // Export: one thread per slot of one limiter's table; every bucket live at `now` becomes one
 // Redis-layout entry (SW: "rl:<key>:<W>" counters, deadline last INCR + w; TB: "tb:<key>",
@@ -2212,6 +2403,8 @@ static void unpermute_mid(const UnpermArgs& a, hipStream_t s) {
 
 hipError_t launch_unpermute(const UnpermArgs& a_in, int res_bytes, hipStream_t s) {
     UnpermArgs a = a_in;
+    a.res_final = a.res;
+    a.pos1_final = a.pos1;
     if (a.pos1 && a.mid && !a.tokens_out && a.n) {      // two-pass: undo pass 1, then pass 0
         if (res_bytes == 8) unpermute_mid<uint64_t>(a, s);
         else if (res_bytes == 1) unpermute_mid<uint8_t>(a, s);

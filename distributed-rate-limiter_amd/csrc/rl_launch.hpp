@@ -25,8 +25,8 @@ struct BatchCtl {
     int64_t base_ms;           // compact records: now_ms = base_ms + now_rel
     uint64_t min_now_key;      // ordered-unsigned encoding of min now_ms
     uint64_t max_now_key;
-    uint32_t span_overflow;    // compact: some now_ms outside [base, base + 2^32)
-    uint32_t pad;
+    uint32_t span_overflow;    // compact: some valid request's now_ms outside [base, base + 2^32)
+    uint32_t n_esc;            // results stored through kResEscape (exact value in `ext`)
     unsigned long long allowed;
     unsigned long long distinct;
     unsigned long long invalid;
@@ -71,6 +71,7 @@ struct RegionArgs {
     const uint8_t* region_lim; // [P]
     const DevLimiter* lims;
     void* res;                 // packed results in region order (u32 compact, u64 wide)
+    int64_t* ext;              // remaining of results stored as kResEscape (same positions)
     double* tok;               // nullable: TB fp64 balances in region order
     BatchCtl* ctl;
     uint32_t n_regions;        // multiple of kRegionsPerBin; one workgroup per bin
@@ -133,6 +134,10 @@ struct UnpermArgs {
     const void* res;
     const double* tok;         // nullable
     void* mid;                 // nullable: n results of scratch (two-pass batches)
+    const int64_t* ext;        // escaped remainders, indexed like res (before `mid`)
+    const BatchCtl* ctl;       // n_esc > 0: fix the escaped results up after the gather
+    const void* res_final;     // (set by launch_unpermute) res and pos1 as the region stage
+    const uint32_t* pos1_final;//  left them, for the escape fix-up
     uint8_t* allowed;
     int64_t* remaining;
     double* tokens_out;        // nullable
@@ -229,5 +234,29 @@ hipError_t launch_route_fold_w(uint32_t n, const uint8_t* allowed, const int64_t
                                void* packed, int width, hipStream_t s);
 hipError_t launch_route_unpack_w(uint32_t n, const uint32_t* perm, const void* packed, int width,
                                  uint8_t* allowed, int64_t* remaining, hipStream_t s);
+// Segmented return trip (rl_route_fold_return / rl_route_unpack_return).
+inline uint64_t ret_block_bytes(uint32_t cap) { return 8 + 16 * (uint64_t)cap; }
+// off[s] / end[s] of segment s for counts[0..n_seg) requests of `width` bytes; returns the
+// total bytes (every segment: its packed results padded to 8 B, then its exception block).
+inline uint64_t ret_layout(const uint64_t* counts, uint32_t n_seg, int width, uint32_t cap,
+                           uint64_t* off, uint32_t* end) {
+    uint64_t o = 0, e = 0;
+    for (uint32_t s = 0; s < n_seg; ++s) {
+        if (off) off[s] = o;
+        e += counts[s];
+        if (end) end[s] = (uint32_t)e;
+        o += ((counts[s] * (uint64_t)width + 7) & ~7ULL) + ret_block_bytes(cap);
+    }
+    return o;
+}
+hipError_t launch_route_fold_ret(uint32_t m, const uint8_t* allowed, const int64_t* remaining,
+                                 void* out, int width, uint32_t n_seg, const uint64_t* counts,
+                                 uint32_t cap, hipStream_t s);
+hipError_t launch_route_unpack_ret(uint32_t n, const uint32_t* perm, const void* in, int width,
+                                   uint32_t n_seg, const uint64_t* counts, uint32_t cap,
+                                   uint8_t* allowed, int64_t* remaining, uint32_t* lost,
+                                   hipStream_t s);
+hipError_t launch_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride,
+                                   hipStream_t s);
 
 }  // namespace rl

@@ -76,8 +76,13 @@ void GpuRateLimiter::checkStatus(int st, const char* where) {
 // Leader-based micro-batcher: the first caller that finds no flush in progress waits
 // `windowMicros_` for company, then runs every queued request as ONE engine batch in
 // queue (arrival) order; the others sleep until their result is filled in.
+// The request's clock is read here, under mu_, so queue order is clock order: two threads
+// on one key can never enqueue their `now` values out of order (the engine's sliding
+// window keeps a key's two newest buckets and assumes a key's time does not run
+// backwards by more than a window).
 void GpuRateLimiter::submit(Pending& p) {
     std::unique_lock<std::mutex> lk(mu_);
+    p.now = clock_();
     queue_.push_back(&p);
     while (!p.done) {
         if (!flushing_) {
@@ -123,7 +128,7 @@ void GpuRateLimiter::flushLocked(std::unique_lock<std::mutex>& lk) {
 
 bool GpuRateLimiter::tryAcquire(const std::string& key, int permits) {
     if (permits <= 0) throw IllegalArgumentException("permits must be positive");  // :87-89 / :106-108
-    Pending p{keyHash(key), permits, clock_(), RL_OP_ACQUIRE};
+    Pending p{keyHash(key), permits, 0, RL_OP_ACQUIRE};
     submit(p);
     if (p.allowed) allowedRequests.increment();
     else rejectedRequests.increment();
@@ -131,13 +136,13 @@ bool GpuRateLimiter::tryAcquire(const std::string& key, int permits) {
 }
 
 int64_t GpuRateLimiter::getAvailablePermits(const std::string& key) {
-    Pending p{keyHash(key), 1, clock_(), RL_OP_PEEK};
+    Pending p{keyHash(key), 1, 0, RL_OP_PEEK};
     submit(p);
     return p.remaining;
 }
 
 void GpuRateLimiter::reset(const std::string& key) {
-    Pending p{keyHash(key), 1, clock_(), RL_OP_RESET};
+    Pending p{keyHash(key), 1, 0, RL_OP_RESET};
     submit(p);
 }
 
@@ -149,9 +154,17 @@ void GpuRateLimiter::tryAcquireBatch(size_t n, const uint64_t* keyHash, const in
     std::vector<int64_t> rem(n);
     int st;
     {
-        std::lock_guard<std::mutex> lk(mu_);        // keep arrival order with single calls
+        // keep arrival order with single calls: wait out a flush in progress (it runs with
+        // mu_ released) and hold the flush slot while this batch runs
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !flushing_; });
+        flushing_ = true;
+        lk.unlock();
         st = rl_try_acquire_batch(engine_->handle(), n, keyHash, permits, nowNanos, lim.data(),
                                   al.data(), rem.data(), nullptr);
+        lk.lock();
+        flushing_ = false;
+        cv_.notify_all();
     }
     checkStatus(st, "tryAcquireBatch");
     uint64_t ok = 0;

@@ -42,7 +42,8 @@ EXPORTS = [
     "rl_route_pack", "rl_route_fold", "rl_route_unpack", "rl_debug_fetch",
     "rl_route_pack_wire", "rl_route_unwire", "rl_result_width", "rl_route_fold_packed",
     "rl_route_unpack_packed", "rl_export_state", "rl_import_state",
-    "rl_sweep_expired",
+    "rl_sweep_expired", "rl_route_return_bytes", "rl_route_fold_return",
+    "rl_route_unpack_return", "rl_route_partition_device",
 ]
 STATE_SW_BUCKET, STATE_TB_BUCKET = 0, 1
 # rl_state_entry (include/rl_engine.h): one live Redis key ("rl:<key>:<W>" / "tb:<key>")
@@ -89,10 +90,9 @@ _lib = None
 
 def build(force: bool = False) -> str:
     """Compile librl_engine.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
-    if force or not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-j4", "-C", PKG_DIR])
-    else:
-        subprocess.check_call(["make", "-s", "-j4", "-C", PKG_DIR])
+    if force:
+        subprocess.check_call(["make", "-s", "-C", PKG_DIR, "clean"])
+    subprocess.check_call(["make", "-s", "-j4", "-C", PKG_DIR])    # make skips up-to-date targets
     return LIB_PATH
 
 
@@ -147,6 +147,11 @@ def lib():
     L.rl_export_state.argtypes = [vp, i64, vp, sz, ctypes.POINTER(sz)]
     L.rl_import_state.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.rl_sweep_expired.argtypes = [vp, i64, ctypes.POINTER(ctypes.c_uint64)]
+    L.rl_route_return_bytes.argtypes = [u32, vp, ctypes.c_int, u32]
+    L.rl_route_return_bytes.restype = ctypes.c_uint64
+    L.rl_route_fold_return.argtypes = [vp, sz, vp, vp, vp, ctypes.c_int, u32, vp, u32, vp]
+    L.rl_route_unpack_return.argtypes = [vp, sz, vp, vp, ctypes.c_int, u32, vp, u32, vp, vp, vp, vp]
+    L.rl_route_partition_device.argtypes = [vp, sz, vp, u32, vp, vp, sz, vp]
     _lib = L
     return L
 
@@ -177,6 +182,15 @@ def mix64(x):
         x = x * np.uint64(0x94D049BB133111EB)
         x = x ^ (x >> np.uint64(31))
     return x
+
+
+def key_hash(key: str) -> int:
+    """String -> 64-bit key hash as the C++ host API computes it (host/ratelimiter.cpp
+    keyHash: FNV-1a 64 over the UTF-8 bytes, then the splitmix64 finaliser)."""
+    h = 0xCBF29CE484222325
+    for c in key.encode("utf-8"):
+        h = ((h ^ c) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return int(mix64(np.uint64(h)))
 
 
 def owner_of(keys, shard_count: int):
@@ -400,6 +414,34 @@ class Engine:
                                             _p(remaining), _p(stream))
         if st != RL_OK:
             raise RlError(st, "rl_route_unpack_packed")
+
+    def route_return_bytes(self, seg_counts, width, exc_cap):
+        c = np.ascontiguousarray(seg_counts, dtype=np.uint64)
+        return int(self._L.rl_route_return_bytes(len(c), c.ctypes.data, width, exc_cap))
+
+    def route_fold_return(self, m, allowed, remaining, out, width, seg_counts, exc_cap,
+                          stream=None):
+        c = np.ascontiguousarray(seg_counts, dtype=np.uint64)
+        st = self._L.rl_route_fold_return(self._h, m, _p(allowed), _p(remaining), _p(out), width,
+                                          len(c), c.ctypes.data, exc_cap, _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_fold_return")
+
+    def route_unpack_return(self, n, perm, inp, width, seg_counts, exc_cap, allowed, remaining,
+                            lost, stream=None):
+        c = np.ascontiguousarray(seg_counts, dtype=np.uint64)
+        st = self._L.rl_route_unpack_return(self._h, n, _p(perm), _p(inp), width, len(c),
+                                            c.ctypes.data, exc_cap, _p(allowed), _p(remaining),
+                                            _p(lost), _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_unpack_return")
+
+    def route_partition_device(self, n, keys_dev, perm_dev, shard_count, counts_dev, stride,
+                               stream=None):
+        st = self._L.rl_route_partition_device(self._h, n, _p(keys_dev), shard_count, _p(perm_dev),
+                                               _p(counts_dev), stride, _p(stream))
+        if st != RL_OK:
+            raise RlError(st, "rl_route_partition_device")
 
     def synth_trace(self, n, keys, permits, now_ns, limiter, *, seed, n_keys, dist=DIST_UNIFORM,
                     zipf_s=1.1, permits_max=4, t0_ns=1_700_000_000_000 * 1_000_000,

@@ -276,6 +276,29 @@ int  rl_route_fold_packed(rl_engine* e, size_t n, const uint8_t* allowed, const 
 int  rl_route_unpack_packed(rl_engine* e, size_t n, const uint32_t* perm, const void* packed,
                             int width, uint8_t* allowed, int64_t* remaining, void* stream);
 
+/* Segmented return trip (the router's default): the decisions for peer s travel as
+ *   [ packed results, seg_counts[s] x width bytes, padded to 8 B ][ exception block ]
+ * with exception block = { u64 count, exc_cap x (i64 position, i64 remaining) } listing the
+ * results whose remaining does not fit the width (token-bucket balances below -3 after
+ * time regression, Lua :56-58). Segment s covers requests [sum(seg_counts[<s]), +seg_counts[s]).
+ * rl_route_return_bytes = total bytes of that layout (0 on bad arguments).
+ * rl_route_unpack_return scatters through perm like rl_route_unpack_packed and adds to
+ * *lost (device u32) the escaped results whose block overflowed (they read
+ * RL_REMAINING_ERROR). */
+uint64_t rl_route_return_bytes(uint32_t n_seg, const uint64_t* seg_counts, int width,
+                               uint32_t exc_cap);
+int  rl_route_fold_return(rl_engine* e, size_t m, const uint8_t* allowed, const int64_t* remaining,
+                          void* out, int width, uint32_t n_seg, const uint64_t* seg_counts,
+                          uint32_t exc_cap, void* stream);
+int  rl_route_unpack_return(rl_engine* e, size_t n, const uint32_t* perm, const void* in, int width,
+                            uint32_t n_seg, const uint64_t* seg_counts, uint32_t exc_cap,
+                            uint8_t* allowed, int64_t* remaining, uint32_t* lost, void* stream);
+/* rl_route_partition without a host round-trip: counts[s] (int64) land in DEVICE memory at
+ * counts_dev[s * counts_stride] (the router's header column), on `stream`. */
+int  rl_route_partition_device(rl_engine* e, size_t n, const uint64_t* key_hash,
+                               uint32_t shard_count, uint32_t* perm, int64_t* counts_dev,
+                               size_t counts_stride, void* stream);
+
 /* ---- synthetic traces (bench / tests; deterministic in (seed, index)) ------ */
 #define RL_DIST_UNIFORM 0
 #define RL_DIST_ZIPF    1

@@ -10,6 +10,11 @@ never computed by an oracle. Provenance:
              (/root/reference/src/test/java/com/ratelimiter/algorithms/
               SlidingWindowRateLimiterTest.java, @Disabled upstream) as traces
              through a real keyspace with a pinned clock.
+  * "doc:*"  the only outputs the reference itself publishes for this path:
+             README.md:83-95 and API_EXAMPLES.md:39-101 (api 100/min -> remaining
+             97 after three requests, 0 once exceeded; login 10/min -> 7 after three;
+             burst token bucket cap 50 at 10/s, batch of 20 -> tokens_remaining 30).
+             These pin SW and TB against reference-held artefacts.
   * "hand:*" hand-derived edge cases from SURVEY.md §8(c): window boundaries,
              Redis TTL lapse, TB expiry, early reject, negative elapsed, and
              traces where an FMA-contracted implementation would differ from
@@ -294,6 +299,67 @@ def kats():
     for i, (seq, why) in enumerate(flips):
         reqs = [req(40 + i, p, t) for (t, p) in seq]
         out.append(case(f"hand:tb:fmaFlip{i}", why, TBL, reqs, lua_expect(seq)))
+
+    # time regression (front-ends with skewed clocks): Redis keys every window separately
+    reqs = [req(60, 1, W + 990) for _ in range(3)] + [req(60, 1, W + 1005), req(60, 1, W + 995),
+                                                      req(60, 1, W + 1010)]
+    # W+990 x3: fresh key -> 9, 8, 7. W+1005: prev = bucket W = 3 (alive to W+1990),
+    # pw = 0.995, 3*0.995 = 2.985 -> est 2, allow, after trunc(3.985) = 3 -> 7.
+    # W+995 (back into window W): curr = bucket W = 3, prev = bucket W-1000 absent -> est 3,
+    # allow, INCR bucket W -> 4 (bucket W+1000 untouched) -> 6.
+    # W+1010: curr = 1, prev = bucket W = 4 (alive to W+1995), pw = 0.99, 3.96 + 1 -> 4,
+    # allow -> curr 2, trunc(5.96) = 5 -> 5.
+    exp = [[1, 9, None], [1, 8, None], [1, 7, None], [1, 7, None], [1, 6, None], [1, 5, None]]
+    out.append(case(
+        "hand:sw:regressionPrevWindow",
+        "a request whose now falls back into the previous window INCRs that window's bucket"
+        " (RedisRateLimitStorage.java:38-49 keys by window start, :185-188) and leaves the"
+        " newer bucket intact; the next request in the newer window weights the grown bucket.",
+        [[SW, 10, 1000, 0.0]], reqs, exp))
+
+    # a drained bucket read 1000 ms, 500 ms and 100 s before its last refill: the Lua reply
+    # integer of a negative balance (tokens - 10, -5, -1000) — below the packed result range
+    reqs = [req(35, 50, T0), req(35, 1, T0 - 1000), req(35, 1, T0 - 500),
+            req(35, 1, T0 - 100_000), req(35, 0, T0 - 300, op=1), req(35, 1, T0 + 100)]
+    exp = [[1, 0, 0.0], [0, -10, -10.0], [0, -5, -5.0], [0, -1000, -1000.0], [0, -3, -3.0],
+           [1, 0, 0.0]]
+    out.append(case(
+        "hand:tb:deepNegative",
+        "elapsed < 0 is not clamped (Lua :56-58): the balance and its reply integer go far"
+        " below zero; nothing is persisted on deny (:66-67), so T0+100 refills from 0.",
+        TBL, reqs, exp))
+
+    # ---------- documented outputs of the reference (README / API_EXAMPLES) ----------
+    API = [[SW, 100, 60000, 0.0]]     # apiRateLimiter, RateLimiterConfig.java:51-56
+    AUTH = [[SW, 10, 60000, 0.0]]     # authRateLimiter, RateLimiterConfig.java:70-74
+    BURST = [[TB, 50, 60000, 10.0]]   # burstRateLimiter, RateLimiterConfig.java:88-92
+    Wa = W60 + 60000
+    out.append(case(
+        "doc:apiRemaining97",
+        "API_EXAMPLES.md:39-47 / README.md:83-88: GET /api/data as one user, the third"
+        " request answers remaining 97 = getAvailablePermits after tryAcquire"
+        " (DemoController.java:45-51). The api limiter's local cache only short-circuits at"
+        " >= maxPermits (SlidingWindowRateLimiter.java:95), so it does not change this.",
+        API, [req(70, 1, Wa + 1000) for _ in range(3)],
+        [[1, 99, None], [1, 98, None], [1, 97, None]]))
+    reqs = [req(71, 1, Wa + 2000) for _ in range(101)]
+    out.append(case(
+        "doc:rateLimitExceededRemaining0",
+        "API_EXAMPLES.md:50-56 / README.md:90-95: past 100 requests in the minute the 429"
+        " body reports remaining 0 (DemoController.java:131-135).",
+        API, reqs, [[1, 99 - i, None] for i in range(100)] + [[0, 0, None]]))
+    out.append(case(
+        "doc:loginRemainingAttempts7",
+        "API_EXAMPLES.md:61-77: POST /api/login (10/min, no cache) answers"
+        " remaining_attempts 7 on the third attempt (DemoController.java:67-75).",
+        AUTH, [req(72, 1, Wa + 3000) for _ in range(3)],
+        [[1, 9, None], [1, 8, None], [1, 7, None]]))
+    out.append(case(
+        "doc:batchTokensRemaining30",
+        "API_EXAMPLES.md:84-101: POST /api/batch size 20 on a fresh bucket (cap 50, 10/s)"
+        " answers tokens_remaining 30 (DemoController.java:92-99): the Lua reply"
+        " {1, 50 - 20} and the build-defined peek right after it.",
+        BURST, [req(73, 20, T0), req(73, 0, T0, op=1)], [[1, 30, 30.0], [0, 30, 30.0]]))
     return out
 
 

@@ -1,0 +1,132 @@
+"""Parity on the bench's exact workloads (BASELINE.json configs; bench.py CONFIGS).
+
+Every case draws its requests from the very generator bench.py times (k_synth, same seed,
+key population, Zipf exponent, permits and time axis as a default `bench.py --config X`
+run), runs them through the HIP path in several batches, and compares every decision and
+remaining bit-exactly with the C oracle (key-sharded over 16 host threads):
+
+* mixed_tenants (configs[3]): the 10-limiter set, 16M requests in 2 batches — two
+  partition passes (1.3M regions), the hot path (top key ~10% of the traffic) and
+  10 limiters with TB + SW, 1-byte and 2-byte results;
+* zipf_1b (configs[4]): TB(50, 10/s) + SW(1000/min), 16M requests in 2 batches;
+* sw_zipf (configs[2]): ONE full 256M-request batch, so the hot chain of its top region
+  (~29.8M records) is compared end to end, not a prefix;
+* config 1 (configs[0], RateLimiterBenchmark.java:48-71): the single-key SW 100000/min
+  stream of 100,000 tryAcquire("user123"), as one batch and as 100 batches.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import rl_amd
+from oracle.coracle import COracle
+from test_gpu_parity import NS, T0, assert_same
+
+pytestmark = pytest.mark.gpu
+
+ORACLE_THREADS = 16
+
+
+def bench_configs():
+    import bench
+    return bench.CONFIGS, bench.T0_NS
+
+
+def synth(eng, cfg, t0_ns, n, index_base=0, steps=13):
+    """The first n requests of a default bench run's step 0 (warmup 3 + steps 10), i.e.
+    bench.py's synth_trace call with ws = 1."""
+    dev = torch.device("cuda", 0)
+    batch = cfg["batch"]
+    n_lim = len(cfg["limiters"])
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    permits = torch.empty(n, dtype=torch.int32, device=dev)
+    now = torch.empty(n, dtype=torch.int64, device=dev)
+    lim = torch.empty(n, dtype=torch.int16, device=dev) if n_lim > 1 else None
+    eng.synth_trace(n, keys, permits, now, lim, seed=cfg["seed"], n_keys=cfg["n_keys"],
+                    dist=cfg["dist"], zipf_s=cfg.get("zipf_s", 1.1),
+                    permits_max=cfg["permits_max"], t0_ns=t0_ns, span_ns=cfg["span_ns"] * steps,
+                    index_base=index_base, n_total=steps * batch, n_limiters=n_lim)
+    return keys, permits, now, lim
+
+
+def run_config(name, n, batches):
+    cfgs, t0_ns = bench_configs()
+    cfg = cfgs[name]
+    per = (n + batches - 1) // batches
+    eng = rl_amd.Engine(device=0, max_batch=per, capacity=cfg["capacity"])
+    for l in cfg["limiters"]:
+        eng.add_limiter(*l)
+    keys, permits, now, lim = synth(eng, cfg, t0_ns, n)
+    allowed = torch.empty(n, dtype=torch.uint8, device="cuda")
+    remaining = torch.empty(n, dtype=torch.int64, device="cuda")
+    for b in range(batches):
+        sl = slice(b * per, min(n, (b + 1) * per))
+        m = sl.stop - sl.start
+        eng.execute_device(m, keys[sl], permits[sl], now[sl], None if lim is None else lim[sl],
+                           None, allowed[sl], remaining[sl])
+        assert eng.last_status() == rl_amd.RL_OK, rl_amd.strerror(eng.last_status())
+    eng.sync()
+    st = eng.stats()
+    k = keys.cpu().numpy().view(np.uint64)
+    p = permits.cpu().numpy()
+    t = now.cpu().numpy()
+    li = None if lim is None else lim.cpu().numpy().view(np.uint16)
+    got = (allowed.cpu().numpy(), remaining.cpu().numpy(), None)
+    del keys, permits, now, lim, allowed, remaining
+    eng.close()
+    o = COracle(cfg["limiters"], nthreads=ORACLE_THREADS)
+    want = o.run(k, p, t, li, None, want_tokens=False)
+    o.close()
+    assert_same(got, want, name)
+    return k, got, st
+
+
+def test_config_mixed_tenants_16m():
+    k, got, st = run_config("mixed_tenants", 1 << 24, 2)
+    _, c = np.unique(k, return_counts=True)
+    assert c.max() > 16384                       # the hot path fired (hot_threshold)
+    assert 0 < got[0].sum() < len(k)
+
+
+def test_config_zipf_1b_16m():
+    k, got, _ = run_config("zipf_1b", 1 << 24, 2)
+    assert 0 < got[0].sum() < len(k)
+
+
+@pytest.mark.timeout(400)
+def test_config_sw_zipf_full_batch():
+    cfgs, _ = bench_configs()
+    n = cfgs["sw_zipf"]["batch"]                 # 2^28: one whole bench batch
+    k, got, _ = run_config("sw_zipf", n, 1)
+    _, c = np.unique(k, return_counts=True)
+    assert c.max() > 25_000_000                  # the ~29.8M-record hot chain, end to end
+
+
+def config1_trace():
+    """RateLimiterBenchmark.benchmarkSlidingWindow_SingleKey (:48-71): 10 threads x 10,000
+    tryAcquire("user123"), maxPermits 100000 per minute; arrivals 12.5 us apart (the
+    published 80,192 req/s run took ~1.25 s, README.md:174-181)."""
+    n = 100_000
+    t0 = (T0 // 60000) * 60000 + 5000
+    keys = np.full(n, rl_amd.key_hash("user123"), np.uint64)
+    now = (t0 * NS + np.arange(n, dtype=np.int64) * 12_500).astype(np.int64)
+    return keys, np.ones(n, np.int32), now
+
+
+def test_config1_single_key_stream():
+    lims = [[rl_amd.SW, 100_000, 60_000, 0.0]]
+    keys, permits, now = config1_trace()
+    want = COracle(lims).run(keys, permits, now, want_tokens=False)
+    assert want[0].sum() == 100_000 and want[1][-1] == 0     # README.md:179: 100% success
+    for batches in (1, 100):
+        e = rl_amd.Engine(max_batch=1 << 17, capacity=1 << 10)
+        e.add_limiter(*lims[0])
+        got = [[], []]
+        for sl in np.array_split(np.arange(len(keys)), batches):
+            a, r, _, st = e.execute(keys[sl], permits[sl], now[sl], want_tokens=False)
+            assert st == rl_amd.RL_OK
+            got[0].append(a); got[1].append(r)
+        assert_same((np.concatenate(got[0]), np.concatenate(got[1]), None), want[:3],
+                    f"config1 x{batches}")

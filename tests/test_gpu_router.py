@@ -16,19 +16,23 @@ NS = 1_000_000
 T0 = 1_700_000_000_000
 
 
-def _trace(steps, world, n):
+def _trace(steps, world, n, regress=False):
     import rl_amd
     rng = np.random.default_rng(7)
     total = steps * world * n
     ranks = np.minimum(rng.zipf(1.2, total), 100_000) - 1
     keys = rl_amd.mix64(ranks.astype(np.uint64))
     permits = rng.integers(1, 5, total).astype(np.int32)
-    now = (T0 * NS + np.sort(rng.integers(0, 30_000 * NS, total))).astype(np.int64)
+    t = np.sort(rng.integers(0, 30_000 * NS, total))
     lim = (ranks % 2).astype(np.uint16)                  # each key belongs to one limiter
+    if regress:            # TB keys (limiter 0): late arrivals -> balances far below zero
+        late = (lim == 0) & (rng.random(total) < 0.05)
+        t[late] -= rng.integers(0, 20_000 * NS, late.sum())
+    now = (T0 * NS + t).astype(np.int64)
     return keys, permits, now, lim
 
 
-def _worker(rank, world, port, steps, n, out, lims):
+def _worker(rank, world, port, steps, n, out, lims, regress=False):
     import rl_amd
     from rl_amd.router import DeviceOps, Router
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -41,7 +45,7 @@ def _worker(rank, world, port, steps, n, out, lims):
         eng.add_limiter(*l)
     ops = DeviceOps(eng, world, dev, n)
     router = Router(ops, world, rank, exchange_device="cpu")
-    keys, permits, now, lim = _trace(steps, world, n)
+    keys, permits, now, lim = _trace(steps, world, n, regress)
     res_a, res_r = [], []
     for s in range(steps):
         sl = slice((s * world + rank) * n, (s * world + rank + 1) * n)
@@ -55,6 +59,7 @@ def _worker(rank, world, port, steps, n, out, lims):
         eng.sync()
         res_a.append(a.cpu().numpy())
         res_r.append(r.cpu().numpy())
+    assert router.finish() == rl_amd.RL_OK
     assert eng.last_status() == rl_amd.RL_OK
     top = (max(l[1] for l in lims) + 3) * 2 + 1
     assert ops.result_width() == (1 if top < 256 else 2 if top < 65536 else 4)
@@ -62,11 +67,12 @@ def _worker(rank, world, port, steps, n, out, lims):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("lims,width", [
-    ([[1, 50, 60000, 10.0], [0, 30, 5000, 0.0]], 1),           # decisions return as 1 B
-    ([[1, 500, 60000, 10.0], [0, 40000, 5000, 0.0]], 4),       # ... and as 4 B
+@pytest.mark.parametrize("lims,width,regress", [
+    ([[1, 50, 60000, 10.0], [0, 30, 5000, 0.0]], 1, False),    # decisions return as 1 B
+    ([[1, 500, 60000, 10.0], [0, 40000, 5000, 0.0]], 4, False),  # ... and as 4 B
+    ([[1, 50, 60000, 10.0], [0, 30, 5000, 0.0]], 1, True),     # + exception blocks
 ])
-def test_two_shards_one_gpu(tmp_path, lims, width):
+def test_two_shards_one_gpu(tmp_path, lims, width, regress):
     from oracle.coracle import COracle
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -74,12 +80,14 @@ def test_two_shards_one_gpu(tmp_path, lims, width):
     s.close()
     world, steps, n = 2, 3, 100_000
     out = str(tmp_path / "r")
-    mp.spawn(_worker, args=(world, port, steps, n, out, lims), nprocs=world, join=True)
-    keys, permits, now, lim = _trace(steps, world, n)
+    mp.spawn(_worker, args=(world, port, steps, n, out, lims, regress), nprocs=world, join=True)
+    keys, permits, now, lim = _trace(steps, world, n, regress)
     top = (max(l[1] for l in lims) + 3) * 2 + 1
     assert width == (1 if top < 256 else 2 if top < 65536 else 4)
     wa, wr, _, _ = COracle(lims).run(
         keys, permits, now, lim, want_tokens=False)
+    if regress:
+        assert (wr < -3).sum() > 100
     for rank in range(world):
         d = np.load(f"{out}.{rank}.npz")
         for st in range(steps):

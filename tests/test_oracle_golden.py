@@ -41,7 +41,10 @@ def test_kat_coverage():
     for must in ["ref:shouldAllowRequestsUnderLimit", "ref:shouldRejectWhenLimitExceeded",
                  "ref:shouldHandleMultiplePermits", "ref:shouldReportAvailablePermits",
                  "ref:shouldResetLimits", "ref:shouldRejectInvalidPermits",
-                 "hand:sw:fmaDiscriminator", "hand:tb:expiryBoundary", "hand:tb:fmaFlip0"]:
+                 "hand:sw:fmaDiscriminator", "hand:tb:expiryBoundary", "hand:tb:fmaFlip0",
+                 "doc:apiRemaining97", "doc:rateLimitExceededRemaining0",
+                 "doc:loginRemainingAttempts7", "doc:batchTokensRemaining30",
+                 "hand:sw:regressionPrevWindow", "hand:tb:deepNegative"]:
         assert must in names
 
 

@@ -12,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import rl_amd
-from rl_amd.router import Router
+from rl_amd.router import EXC_CAP, Router
 from oracle.coracle import COracle
 
 NS = 1_000_000
@@ -24,15 +24,89 @@ _NP_W = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}
 _NP_U = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}
 
 
+def ret_layout(counts, width):
+    """Byte offsets of the segmented return layout (include/rl_engine.h rl_route_fold_return)."""
+    offs, o = [], 0
+    for c in counts:
+        offs.append(o)
+        o += (c * width + 7) // 8 * 8 + 8 + 16 * EXC_CAP
+    return offs, o
+
+
 class HostOps:
     def __init__(self, world):
         self.world = world
         self.o = COracle(LIMS)
+        self._lost = 0
 
-    def partition(self, n, keys):
+    def header(self):
+        return torch.zeros((self.world, 4), dtype=torch.int64)
+
+    def partition(self, n, keys, hdr):
         own = rl_amd.owner_of(keys.numpy().view(np.uint64), self.world)
         self.perm = np.argsort(own, kind="stable")
-        return np.bincount(own, minlength=self.world).tolist()
+        hdr[:, 0] = torch.from_numpy(np.bincount(own, minlength=self.world).astype(np.int64))
+
+    def engine_status(self):
+        return rl_amd.RL_OK
+
+    def lost(self):
+        return self._lost
+
+    def return_bytes(self, counts, width):
+        return ret_layout(counts, width)[1]
+
+    def decide_return(self, m, k, p, t, lim, width, src_counts):
+        kk = k.numpy().view(np.uint64)
+        lm = None if lim is None else lim.numpy().view(np.uint16)
+        a, r, _, _ = self.o.run(kk, p.numpy(), t.numpy(), lm, None, want_tokens=False)
+        offs, tot = ret_layout(src_counts, width)
+        out = np.zeros(tot, np.uint8)
+        hi = (((1 << (8 * width)) - 1) >> 1) - 3
+        beg = 0
+        for s, c in enumerate(src_counts):
+            aa, rr = a[beg:beg + c].astype(np.int64), r[beg:beg + c]
+            fits = (rr >= -3) & (rr <= hi)
+            v = np.where(fits, ((rr + 3) << 1) | aa, 1).astype(_NP_U[width])
+            out[offs[s]:offs[s] + c * width] = v.view(np.uint8)
+            blk = out[offs[s] + (c * width + 7) // 8 * 8:][:8 + 16 * EXC_CAP].view(np.int64)
+            esc = np.nonzero(~fits)[0]
+            blk[0] = len(esc)
+            take = esc[:EXC_CAP]
+            blk[1:1 + 2 * len(take):2] = take
+            blk[2:2 + 2 * len(take):2] = rr[take]
+            beg += c
+        self.escapes = getattr(self, "escapes", 0) + int((~((r >= -3) & (r <= hi))).sum())
+        return torch.from_numpy(out)
+
+    def return_buffer(self, counts, width):
+        return torch.empty(self.return_bytes(counts, width), dtype=torch.uint8)
+
+    def unpack_return(self, n, back, width, counts, allowed, remaining):
+        b = back.numpy()
+        offs, _ = ret_layout(counts, width)
+        a_out = np.empty(n, np.uint8)
+        r_out = np.empty(n, np.int64)
+        beg = 0
+        for s, c in enumerate(counts):
+            v = b[offs[s]:offs[s] + c * width].view(_NP_U[width]).astype(np.int64)
+            a_out[beg:beg + c] = v & 1
+            r_out[beg:beg + c] = (v >> 1) - 3
+            esc = np.nonzero(v == 1)[0]
+            if len(esc):
+                blk = b[offs[s] + (c * width + 7) // 8 * 8:][:8 + 16 * EXC_CAP].view(np.int64)
+                cnt = min(int(blk[0]), EXC_CAP)
+                found = dict(zip(blk[1:1 + 2 * cnt:2].tolist(), blk[2:2 + 2 * cnt:2].tolist()))
+                for j in esc:
+                    a_out[beg + j] = 0
+                    if int(j) in found:
+                        r_out[beg + j] = found[int(j)]
+                    else:
+                        r_out[beg + j] = -3
+                        self._lost += 1
+            beg += c
+        allowed.numpy()[self.perm] = a_out
+        remaining.numpy()[self.perm] = r_out
 
     def pack(self, n, keys, permits, now, limiter=None):
         self.packs_wide = getattr(self, "packs_wide", 0) + 1
@@ -83,21 +157,6 @@ class HostOps:
         t = (np.repeat(np.asarray(bases, np.int64), counts) + rel) * NS
         return torch.from_numpy(w[:, 0].copy()), torch.from_numpy(p.copy()), torch.from_numpy(t)
 
-    def decide_packed(self, m, k, p, t, lim, width):
-        kk = k.numpy().view(np.uint64)
-        lm = None if lim is None else lim.numpy().view(np.uint16)
-        a, r, _, _ = self.o.run(kk, p.numpy(), t.numpy(), lm, None, want_tokens=False)
-        v = ((r + 3) << 1) | a.astype(np.int64)
-        return torch.from_numpy(v.astype(_NP_W[width]))
-
-    def back_buffer_packed(self, n, width):
-        return torch.from_numpy(np.empty(n, _NP_W[width]))
-
-    def unpack_packed(self, n, back, width, allowed, remaining):
-        v = back.numpy().view(_NP_U[width]).astype(np.int64)
-        allowed.numpy()[self.perm] = (v & 1).astype(np.uint8)
-        remaining.numpy()[self.perm] = (v >> 1) - 3
-
 
     def unpack(self, n, back, allowed, remaining):
         b = back.numpy()
@@ -108,21 +167,25 @@ class HostOps:
         pass
 
 
-def global_trace(steps, world, n, span_ms=20_000):
+def global_trace(steps, world, n, span_ms=20_000, regress=False):
     rng = np.random.default_rng(42)
     total = steps * world * n
     ranks = np.minimum(rng.zipf(1.3, total), 5000) - 1
     keys = rl_amd.mix64(ranks.astype(np.uint64))
     permits = rng.integers(1, 5, total).astype(np.int32)
-    now = (T0 * NS + np.sort(rng.integers(0, span_ms * NS, total))).astype(np.int64)
+    t = np.sort(rng.integers(0, span_ms * NS, total))
     lim = (ranks % len(LIMS)).astype(np.uint16)          # each key belongs to one limiter
+    if regress:   # token-bucket keys only: 5% arrive up to 10 s late (deep negative balances)
+        late = (lim == 0) & (rng.random(total) < 0.05)
+        t[late] -= rng.integers(0, 10_000 * NS, late.sum())
+    now = (T0 * NS + t).astype(np.int64)
     return keys, permits, now, lim
 
 
-def _worker(rank, world, port, steps, n, out_path, span_ms=20_000):
+def _worker(rank, world, port, steps, n, out_path, span_ms=20_000, regress=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    keys, permits, now, lim = global_trace(steps, world, n, span_ms)
+    keys, permits, now, lim = global_trace(steps, world, n, span_ms, regress)
     ops = HostOps(world)
     router = Router(ops, world, rank)
     got_a, got_r = [], []
@@ -137,8 +200,9 @@ def _worker(rank, world, port, steps, n, out_path, span_ms=20_000):
         router.step(k, p, t, a, r, li)
         got_a.append(a.numpy().copy())
         got_r.append(r.numpy().copy())
+    assert router.finish() == rl_amd.RL_OK
     np.savez(f"{out_path}.{rank}.npz", a=np.concatenate(got_a), r=np.concatenate(got_r),
-             wide_steps=getattr(ops, "packs_wide", 0))
+             wide_steps=getattr(ops, "packs_wide", 0), escapes=getattr(ops, "escapes", 0))
     dist.destroy_process_group()
 
 
@@ -150,14 +214,19 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,span_ms", [(2, 20_000), (4, 20_000), (2, 1 << 36)])
-def test_router_matches_single_process_oracle(tmp_path, world, span_ms):
+@pytest.mark.parametrize("world,span_ms,regress", [(2, 20_000, False), (4, 20_000, False),
+                                                   (2, 1 << 36, False), (2, 20_000, True),
+                                                   (4, 20_000, True)])
+def test_router_matches_single_process_oracle(tmp_path, world, span_ms, regress):
     """span 2^36 ms: every rank's slice spans more than the 32-bit wire time, so the router falls
-    back to the wide layout (all ranks agree through the header's overflow flags)."""
+    back to the wide layout (all ranks agree through the header's overflow flags).
+    regress: late token-bucket requests drive balances far below zero; their remainders do
+    not fit the 1-byte return width and travel in the exception blocks."""
     steps, n = 3, 3000
     out = str(tmp_path / "res")
-    mp.spawn(_worker, args=(world, _free_port(), steps, n, out, span_ms), nprocs=world, join=True)
-    keys, permits, now, lim = global_trace(steps, world, n, span_ms)
+    mp.spawn(_worker, args=(world, _free_port(), steps, n, out, span_ms, regress), nprocs=world,
+             join=True)
+    keys, permits, now, lim = global_trace(steps, world, n, span_ms, regress)
     wa, wr, _, _ = COracle(LIMS).run(keys, permits, now, lim, None, want_tokens=False)
     for rank in range(world):
         d = np.load(f"{out}.{rank}.npz")
@@ -166,3 +235,7 @@ def test_router_matches_single_process_oracle(tmp_path, world, span_ms):
             assert np.array_equal(d["a"][s * n:(s + 1) * n], wa[sl]), (rank, s)
             assert np.array_equal(d["r"][s * n:(s + 1) * n], wr[sl]), (rank, s)
         assert int(d["wide_steps"]) == (steps if span_ms > 1 << 35 else 0)
+        if regress:
+            assert int(d["escapes"]) > 0
+    if regress:
+        assert (wr < -3).sum() > 50

@@ -74,6 +74,21 @@ def main():
                   "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES"):
             if k in mean:
                 d[k] = mean[k]
+    # the whole step: every kernel of the bench's timed and warmup steps except the
+    # trace generator, divided by the number of steps (unpermute launches)
+    steps = st.get("unpermute", {}).get("calls")
+    tot = collections.defaultdict(float)
+    for f, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        p = f"{base}/{f}/{f}_counter_collection.csv"
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            if "k_synth" not in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                tot[ctr] += float(r["Counter_Value"])
+    if steps and "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
+        st["step"] = {"fetch_bytes": tot["FETCH_SIZE"] * 1024 * 2 / steps,
+                      "write_bytes": tot["WRITE_SIZE"] * 1024 / steps, "steps": steps}
+        st["step"]["hbm_bytes_per_launch"] = st["step"]["fetch_bytes"] + st["step"]["write_bytes"]
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     out[a.config] = st
     out.setdefault("_meta", {})["note"] = (
