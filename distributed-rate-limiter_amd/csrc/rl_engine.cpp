@@ -193,6 +193,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     if (o.shard_count == 0) o.shard_count = 1;
     if ((o.shard_count & (o.shard_count - 1)) != 0 || o.shard_count > 64) return RL_E_INVALID_ARG;
     if (o.shard_index >= o.shard_count) return RL_E_INVALID_ARG;
+    if (o.max_skew_ms < 0) return RL_E_INVALID_ARG;
     rl_engine* e = new (std::nothrow) rl_engine();
     if (!e) return RL_E_NOMEM;
     e->opts = o;
@@ -495,6 +496,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.lims = e->d_lims; ra.res = e->res; ra.ext = e->ext; ra.tok = tokens_after ? e->tok : nullptr;
     ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
+    ra.skew_ms = e->opts.max_skew_ms;
     if (e->debug_regions) {
         if (e->dbg_cap < (size_t)n_bins * kDbgWords) {
             dfree(e->dbg);

@@ -62,6 +62,12 @@ __device__ inline uint64_t ord_key(int64_t v) { return (uint64_t)v ^ 0x800000000
 __device__ inline int64_t batch_lo(const BatchCtl* c) {
     return c->min_now_key == ~0ULL ? INT64_MIN : (int64_t)(c->min_now_key ^ 0x8000000000000000ULL);
 }
+// Time from which a loaded region keeps a slot: every later request has now >= this
+// (batches in global time order, less the caller's declared skew, rl_opts.max_skew_ms).
+__device__ inline int64_t keep_from(const RegionArgs& a) {
+    const int64_t lo = batch_lo(a.ctl);
+    return lo < INT64_MIN + a.skew_ms ? INT64_MIN : lo - a.skew_ms;
+}
 __device__ inline int64_t batch_hi(const BatchCtl* c) {
     return c->max_now_key == 0ULL ? batch_lo(c) : (int64_t)(c->max_now_key ^ 0x8000000000000000ULL);
 }
@@ -660,7 +666,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     const uint32_t region = bin * RPB + rb;
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
-    const int64_t batch_min = batch_lo(a.ctl);
+    const int64_t batch_min = keep_from(a);
     const uint32_t pad = a.n_total + lane;          // padding slot for idle lanes
     const Rec* recs = (const Rec*)a.rec;
     Res* res = (Res*)a.res;
@@ -1142,7 +1148,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 #pragma unroll
         for (uint32_t k = 0; k < NS / 64; ++k) {
             const Slot v = img[k];
-            if (slot_live(L, v, lo)) {
+            if (slot_live(L, v, keep_from(a))) {
                 uint32_t p = slot_home(v.tag);
                 while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
                 S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;

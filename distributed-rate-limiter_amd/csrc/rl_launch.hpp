@@ -79,6 +79,7 @@ struct RegionArgs {
     int32_t shard_bits;
     int32_t bin_shift;
     uint32_t ablate;
+    int64_t skew_ms;           // rl_opts.max_skew_ms: slots kept until dead at batch min - skew
     const uint32_t* rend;      // nullable: bin b holds records [rstart[b], rend[b]) (2 passes)
     // hot regions (bin_shift 0): k_hot_select lists the largest bins (>= hot_threshold
     // records, at most kHotMax); the k_hot_* kernels own them (hot_mark[bin] == epoch),

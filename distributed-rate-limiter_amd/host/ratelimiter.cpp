@@ -29,6 +29,7 @@ GpuEngine::GpuEngine(const Options& o) {
     opts.max_batch = o.maxBatch;
     opts.default_capacity = o.defaultCapacity;
     opts.shard_count = 1;
+    opts.max_skew_ms = o.maxSkewMs;
     int st = rl_create(&opts, &e_);
     if (st != RL_OK) throw StorageException(std::string("rl_create: ") + rl_strerror(st), st);
 }

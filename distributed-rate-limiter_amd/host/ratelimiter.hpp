@@ -102,6 +102,7 @@ class GpuEngine {
         int device = 0;
         uint64_t maxBatch = 1u << 20;
         uint64_t defaultCapacity = 1u << 20;
+        int64_t maxSkewMs = 0;          // rl_opts.max_skew_ms
     };
     explicit GpuEngine(const Options& o);
     GpuEngine() : GpuEngine(Options{}) {}

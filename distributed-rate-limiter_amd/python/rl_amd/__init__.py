@@ -62,7 +62,8 @@ class RlError(RuntimeError):
 class Opts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("max_batch", ctypes.c_uint64), ("default_capacity", ctypes.c_uint64),
-                ("shard_index", ctypes.c_uint32), ("shard_count", ctypes.c_uint32)]
+                ("shard_index", ctypes.c_uint32), ("shard_count", ctypes.c_uint32),
+                ("max_skew_ms", ctypes.c_int64)]
 
 
 class LimiterConfig(ctypes.Structure):
@@ -204,11 +205,12 @@ class Engine:
     """One engine = one GPU's state table + stream (rl_create)."""
 
     def __init__(self, device: int = 0, max_batch: int = 1 << 22, capacity: int = 1 << 20,
-                 stage_timing: bool = False, shard_index: int = 0, shard_count: int = 1):
+                 stage_timing: bool = False, shard_index: int = 0, shard_count: int = 1,
+                 max_skew_ms: int = 0):
         self._L = lib()
         o = Opts(device=device, flags=OPT_STAGE_TIMING if stage_timing else 0,
                  max_batch=max_batch, default_capacity=capacity, shard_index=shard_index,
-                 shard_count=shard_count)
+                 shard_count=shard_count, max_skew_ms=max_skew_ms)
         h = ctypes.c_void_p()
         st = self._L.rl_create(ctypes.byref(o), ctypes.byref(h))
         if st != RL_OK:

@@ -45,7 +45,10 @@ import torch.distributed as dist
 
 import rl_amd
 
-EXC_CAP = 256          # exception entries per (owner, source) pair per step
+# Exception entries per (owner, source) pair per step (16 B each). Beyond that, the
+# decisions stay exact but the extra out-of-range remainders read RL_REMAINING_ERROR and
+# finish() reports RL_E_CAPACITY on every rank.
+EXC_CAP = 4096
 
 
 class RouterError(RuntimeError):
@@ -307,7 +310,7 @@ class Router:
             self._pub = int(self.ops.engine_status())
             self._pending = False
         lost = self.ops.lost()
-        mine = torch.tensor([self._pub if lost == 0 else rl_amd.RL_E_DEVICE], dtype=torch.int64)
+        mine = torch.tensor([self._pub if lost == 0 else rl_amd.RL_E_CAPACITY], dtype=torch.int64)
         dev = self.xdev or (self.ops.dev if hasattr(self.ops, "dev") else "cpu")
         mine = mine.to(dev)
         allst = [torch.empty_like(mine) for _ in range(self.world)]

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 1
+#define RL_ABI_VERSION 2
 
 /* ---- status codes -------------------------------------------------------- */
 #define RL_OK                   0
@@ -93,6 +93,10 @@ typedef struct rl_opts {
     uint64_t default_capacity;  /* expected live keys per limiter when rl_add_limiter is used */
     uint32_t shard_index;       /* multi-GPU: this engine owns keys with owner(h) == shard   */
     uint32_t shard_count;       /* multi-GPU: number of shards (power of two, 1 = no sharding) */
+    int64_t  max_skew_ms;       /* how far a request may lag behind the earliest request of an
+                                   EARLIER batch (front-ends with skewed clocks); state is kept
+                                   until it is dead that long before a batch's earliest now.
+                                   0: batches arrive in global time order */
 } rl_opts;
 
 #define RL_OPT_STAGE_TIMING 0x1u  /* record hipEvents around every stage (rl_stage_times) */

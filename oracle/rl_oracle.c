@@ -129,12 +129,15 @@ static void ks_grow(orc_keyspace* ks) {
     free(old.slots);
 }
 
-/* Lookup honouring lazy expiry: a key is expired iff now > expireAt. */
+/* Lookup: a key is expired (reads as missing) iff now > expireAt — a pure function of
+ * (deadline, now). A read that finds the key expired does not delete it, so a request
+ * arriving later with an EARLIER now (time regression, e.g. skewed front-end clocks) still
+ * sees it; for per-key non-decreasing time this is exactly Redis's lazy deletion. */
 static orc_entry* ks_lookup(orc_keyspace* ks, uint8_t ns, uint16_t lim, uint64_t key,
                             int64_t wstart, int64_t now) {
     orc_entry* e = ks_find_slot(ks, ns, lim, key, wstart);
     if (!e->used || !e->present) return NULL;
-    if (now > e->expire_at) { e->present = 0; return NULL; }
+    if (now > e->expire_at) return NULL;
     return e;
 }
 

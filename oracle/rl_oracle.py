@@ -68,13 +68,13 @@ class Redis:
         self.exp: dict[str, int] = {}
 
     def _alive(self, k: str, now: int) -> bool:
+        # A pure function of (deadline, now): expired iff now > expireAt. The entry is not
+        # deleted when a read finds it expired, so a later-arriving request with an EARLIER
+        # now (time regression) still sees it; under per-key non-decreasing time this is
+        # the same as Redis deleting it (the single logical clock of SURVEY §8(c)).
         if k not in self.kv:
             return False
-        if k in self.exp and now > self.exp[k]:
-            del self.kv[k]
-            del self.exp[k]
-            return False
-        return True
+        return not (k in self.exp and now > self.exp[k])
 
     def get(self, k: str, now: int) -> int:  # RedisRateLimitStorage.get
         return int(self.kv[k]) if self._alive(k, now) else 0

@@ -26,8 +26,8 @@ def _trace(steps, world, n, regress=False):
     t = np.sort(rng.integers(0, 30_000 * NS, total))
     lim = (ranks % 2).astype(np.uint16)                  # each key belongs to one limiter
     if regress:            # TB keys (limiter 0): late arrivals -> balances far below zero
-        late = (lim == 0) & (rng.random(total) < 0.05)
-        t[late] -= rng.integers(0, 20_000 * NS, late.sum())
+        late = (lim == 0) & (rng.random(total) < 0.005)
+        t[late] -= rng.integers(0, 5_000 * NS, late.sum())
     now = (T0 * NS + t).astype(np.int64)
     return keys, permits, now, lim
 
