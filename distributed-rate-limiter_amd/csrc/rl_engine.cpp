@@ -91,6 +91,7 @@ struct rl_engine {
     size_t dbg_cap = 0;
     bool debug_regions = false;
     BatchCtl* d_ctl = nullptr;
+    unsigned long long* d_stats = nullptr;  // [kStatSlots][kStWords] sharded counters (zeroed)
     BatchCtl* h_ctl = nullptr;              // pinned copy of the last batch's ctl
 
     // host-API staging (device copies of caller buffers)
@@ -211,6 +212,9 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     e->timing = (o.flags & RL_OPT_STAGE_TIMING) != 0;
     if (e->timing) ensure_events(e);
     int rc = dalloc(&e->d_ctl, 1);
+    if (rc == RL_OK) rc = dalloc(&e->d_stats, (size_t)kStatSlots * kStWords);
+    if (rc == RL_OK && hipMemset(e->d_stats, 0, (size_t)kStatSlots * kStWords * 8) != hipSuccess)
+        rc = RL_E_DEVICE;
     if (rc == RL_OK && hipHostMalloc((void**)&e->h_ctl, sizeof(BatchCtl)) != hipSuccess) rc = RL_E_NOMEM;
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
     if (rc == RL_OK) rc = dalloc(&e->bin_total, 1u << kMaxDigitBits);
@@ -233,7 +237,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->counts); dfree(e->bin_total); dfree(e->bin_base);
     dfree(e->region_count); dfree(e->region_start);
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
-    dfree(e->d_ctl);
+    dfree(e->d_ctl); dfree(e->d_stats);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
     dfree(e->route_scratch); dfree(e->route_counts);
@@ -497,6 +501,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
     ra.skew_ms = e->opts.max_skew_ms;
+    ra.stats = e->d_stats;
     if (e->debug_regions) {
         if (e->dbg_cap < (size_t)n_bins * kDbgWords) {
             dfree(e->dbg);
@@ -521,6 +526,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     HIP_OK(launch_region(ra, wide, res_bytes, s));       // hot chains first, then the regions
     mark(e, 10);
     if (hot) HIP_OK(launch_hot_fill(ra, wide, res_bytes, s));
+    HIP_OK(launch_stats_reduce(e->d_stats, e->d_ctl, s));
     mark(e, 11);
     mark(e, 8);
     UnpermArgs ua{};

@@ -796,11 +796,12 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         touched += __shfl_xor(touched, off, 64);
     }
     if (lane == 0) {
-        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
-        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
-        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
-        atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
-        atomicAdd(&a.ctl->regions, 1ULL);
+        unsigned long long* st = a.stats + (size_t)(blockIdx.x & (kStatSlots - 1)) * kStWords;
+        if (n_allowed) atomicAdd(st + kStAllowed, (unsigned long long)n_allowed);
+        if (n_invalid) atomicAdd(st + kStInvalid, (unsigned long long)n_invalid);
+        if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
+        atomicAdd(st + kStDistinct, (unsigned long long)touched);
+        atomicAdd(st + kStRegions, 1ULL);
         if (a.dbg) {
             uint64_t* d = a.dbg + (size_t)bin * kDbgWords;
             d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = cnt; d[3] = n_rounds;
@@ -1471,9 +1472,10 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         n_caperr += __shfl_xor(n_caperr, off, 64);
     }
     if (lane == 0) {
-        atomicAdd(&a.ctl->allowed, (unsigned long long)n_allowed);
-        if (n_invalid) atomicAdd(&a.ctl->invalid, (unsigned long long)n_invalid);
-        if (n_caperr) atomicAdd(&a.ctl->cap_err, (unsigned long long)n_caperr);
+        unsigned long long* st = a.stats + (size_t)(blockIdx.x & (kStatSlots - 1)) * kStWords;
+        if (n_allowed) atomicAdd(st + kStAllowed, (unsigned long long)n_allowed);
+        if (n_invalid) atomicAdd(st + kStInvalid, (unsigned long long)n_invalid);
+        if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
     }
     // ---- write the region back, statistics
     __shared__ uint64_t s_w1[2];                      // wave 1's debug counters
@@ -1493,8 +1495,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     }
     for (int off = 32; off > 0; off >>= 1) touched += __shfl_xor(touched, off, 64);
     if (lane == 0) {
-        atomicAdd(&a.ctl->distinct, (unsigned long long)touched);
-        atomicAdd(&a.ctl->regions, 1ULL);
+        unsigned long long* st = a.stats + (size_t)(blockIdx.x & (kStatSlots - 1)) * kStWords;
+        atomicAdd(st + kStDistinct, (unsigned long long)touched);
+        atomicAdd(st + kStRegions, 1ULL);
         if (a.dbg) {
             uint64_t* d = a.dbg + (size_t)region * kDbgWords;
             // top bit: a hot region; bits 0-31: detailed chunks, 32-62: other-key records
@@ -2345,6 +2348,37 @@ static void region_launch(const RegionArgs& a, hipStream_t s) {
         if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 3, false>), g, b, 0, s, a);
         else hipLaunchKernelGGL((k_regions<Codec, Res, false, 3, false>), g, b, 0, s, a);
     }
+}
+
+// Fold the sharded batch counters into BatchCtl and clear them for the next batch.
+__global__ __launch_bounds__(256) void k_stats_reduce(unsigned long long* stats, BatchCtl* ctl) {
+    __shared__ unsigned long long part[kStWords][4];
+    const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    for (uint32_t s = t; s < kStatSlots; s += 256) {
+        unsigned long long* p = stats + (size_t)s * kStWords;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) { acc[k] += p[k]; p[k] = 0; }
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        unsigned long long v = acc[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) part[k][wid] = v;
+    }
+    __syncthreads();
+    if (t < 5) {
+        const unsigned long long v = part[t][0] + part[t][1] + part[t][2] + part[t][3];
+        unsigned long long* dst = t == kStAllowed ? &ctl->allowed : t == kStInvalid ? &ctl->invalid
+                                : t == kStCapErr ? &ctl->cap_err : t == kStDistinct ? &ctl->distinct
+                                : &ctl->regions;
+        *dst += v;
+    }
+}
+
+hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats, ctl);
+    return hipGetLastError();
 }
 
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {

@@ -80,6 +80,7 @@ struct RegionArgs {
     int32_t bin_shift;
     uint32_t ablate;
     int64_t skew_ms;           // rl_opts.max_skew_ms: slots kept until dead at batch min - skew
+    unsigned long long* stats; // [kStatSlots][8] sharded batch counters (k_stats_reduce)
     const uint32_t* rend;      // nullable: bin b holds records [rstart[b], rend[b]) (2 passes)
     // hot regions (bin_shift 0): k_hot_select lists the largest bins (>= hot_threshold
     // records, at most kHotMax); the k_hot_* kernels own them (hot_mark[bin] == epoch),
@@ -100,6 +101,12 @@ constexpr int kMaxShards = 64;              // routing: shards per router
 constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
 constexpr uint32_t kDbgWords = 8;        // debug words per bin
+// Batch counters are sharded: one device-scope atomic word sustains only ~88 adds per us
+// (MI355X_MICROARCH.md, rows 'dequeue' / 'fanin'), and every region wave adds to them, so a
+// 1.3M-region batch on ONE set of words serialises for >10 ms. Region waves add to slot
+// (block id mod kStatSlots), one 64-B line per slot; k_stats_reduce folds them into BatchCtl.
+constexpr uint32_t kStatSlots = 1024;
+enum : uint32_t { kStAllowed = 0, kStInvalid, kStCapErr, kStDistinct, kStRegions, kStWords = 8 };
 
 struct HotInfo {             // one listed hot region
     uint64_t tag;            // its dominant key (mix64 of the key hash)
@@ -202,6 +209,7 @@ hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hi
 hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
                            uint32_t cols, hipStream_t s);
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
+hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s);
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s);   // prep, scan, summaries
 hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
 hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
