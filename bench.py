@@ -126,7 +126,7 @@ def config1_line(dev):
     keys = np.full(n, rl_amd.key_hash("user123"), np.uint64)
     now = (t0 * NS + np.arange(n, dtype=np.int64) * 12_500).astype(np.int64)
     permits = np.ones(n, np.int32)
-    lim = [(rl_amd.SW, 100_000, 60_000, 0.0)]
+    lim = [(rl_amd.SW, 100_000, 60_000, 0.0, 0, 50)]      # cache on, TTL 50 ms (:50-55)
     o = COracle(lim)
     c0 = time.perf_counter()
     oa, orem, _, _ = o.run(keys, permits, now, want_tokens=False)

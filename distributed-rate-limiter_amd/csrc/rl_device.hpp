@@ -59,7 +59,7 @@ constexpr uint32_t kPermitMask = (1u << kPermitBits) - 1;   // 0 = invalid marke
 constexpr int64_t kCompactMaxPermits = (int64_t)kPermitMask - 1;  // clamp is exact below this
 
 // ---------------------------------------------------------------- limiter table
-struct DevLimiter {          // 80 B, read-only during a batch
+struct DevLimiter {          // 96 B, read-only during a batch
     int32_t algo;
     int32_t region_bits;     // k: the limiter has 2^k regions
     uint32_t region_base;    // first global region id
@@ -71,6 +71,8 @@ struct DevLimiter {          // 80 B, read-only during a batch
     double capacity;         // TB: (double)maxPermits (Lua tonumber(ARGV[1]))
     uint64_t table;          // device address of this limiter's region array
     double inv_window;       // 1.0 / w: first guess of Java's now / w (jdiv corrects it)
+    uint64_t cache_table;    // SW local cache: one u64 per slot (block-until ms), or 0
+    int64_t cache_ttl_ms;    // localCacheTtl (0: no local cache, the parity-mode default)
     uint64_t pad1;
 };
 
@@ -225,6 +227,8 @@ struct Outcome {
     int64_t remaining;
     double tokens;           // TB fp64 balance (NaN otherwise)
     uint64_t a, b, c;        // new state when mutate
+    int64_t cval;            // SW: the count the reference would put in its local cache
+    uint64_t x;              // SW local cache: block-until ms after the request (0: none)
 };
 
 // ---------------------------------------------------------------- token bucket
@@ -251,6 +255,7 @@ __device__ inline Outcome tb_step(const DevLimiter& L, uint32_t op, int32_t perm
                                   int64_t now, uint64_t a, uint64_t b, uint64_t c) {
     Outcome o;
     o.mutate = false; o.allowed = false; o.remaining = 0; o.tokens = __builtin_nan("");
+    o.cval = 0; o.x = 0;
     o.a = a; o.b = b; o.c = c;
     if (op == (uint32_t)kOpReset) {                  // DEL tb:key (:153-158)
         o.mutate = true; o.a = 0; o.b = 0; o.c = 0;
@@ -354,6 +359,7 @@ __device__ inline Outcome sw_step_g(const DevLimiter& L, uint32_t op, int32_t pe
                                     uint64_t c) {
     Outcome o;
     o.mutate = false; o.allowed = false; o.remaining = 0; o.tokens = __builtin_nan("");
+    o.cval = 0; o.x = 0;
     o.a = a; o.b = b; o.c = c;
     const int64_t w = L.window_ms;
     SW2 s = sw_unpack(a, b, c);
@@ -368,6 +374,7 @@ __device__ inline Outcome sw_step_g(const DevLimiter& L, uint32_t op, int32_t pe
         return o;
     }
     const int64_t est = sw_estimate(s, geo, now, w);
+    o.cval = est;
     if (op == (uint32_t)kOpPeek || est + (int64_t)permits > L.max_permits) {  // :104
         const int64_t r = L.max_permits - est;
         o.remaining = r > 0 ? r : 0;
@@ -403,11 +410,13 @@ __device__ inline Outcome sw_step_g(const DevLimiter& L, uint32_t op, int32_t pe
         // never rolled back.
         o.mutate = false;
         o.allowed = 1 <= L.max_permits;
+        o.cval = 1;
         const int64_t r = L.max_permits - 1;              // estimate after: 0 * pw + 1
         o.remaining = r > 0 ? r : 0;
         return o;
     }
     o.mutate = true;
+    o.cval = new_count;
     o.allowed = (int64_t)new_count <= L.max_permits;  // :123
     const int64_t est2 = sw_estimate(s, geo, now, w);  // remaining after the request (A4)
     const int64_t r = L.max_permits - est2;
@@ -415,6 +424,32 @@ __device__ inline Outcome sw_step_g(const DevLimiter& L, uint32_t op, int32_t pe
     o.a = (uint64_t)s.b1_start;
     o.b = (uint64_t)s.b1_cnt | ((uint64_t)s.b0_cnt << 32);
     o.c = (uint64_t)(uint32_t)s.b1_off | ((uint64_t)(uint32_t)s.b0_off << 32);
+    return o;
+}
+
+// tryAcquire / reset with the Caffeine local cache on (SlidingWindowRateLimiter.java:93-121,
+// :148-150). The cache entry (value, write time) matters only through x = write time + ttl
+// when value >= maxPermits (0 otherwise): getIfPresent returns it iff now - write < ttl
+// (expireAfterWrite, :57-64) and only a value >= maxPermits short-circuits (:95); every put
+// overwrites. `hit` = rejected from the cache without touching the Redis state.
+__device__ inline Outcome sw_step_cache(const DevLimiter& L, uint32_t op, int32_t permits,
+                                        int64_t now, const SWGeo& geo, uint64_t a, uint64_t b,
+                                        uint64_t c, uint64_t x, bool& hit) {
+    hit = false;
+    if (op == (uint32_t)kOpAcquire && x != 0 && now < (int64_t)x) {           // :93-100
+        Outcome o = sw_step_g(L, kOpPeek, permits, now, geo, a, b, c);     // remaining only
+        hit = true;
+        o.x = x;
+        return o;
+    }
+    Outcome o = sw_step_g(L, op, permits, now, geo, a, b, c);
+    o.x = x;
+    if (op == (uint32_t)kOpReset) {                                            // :148-150
+        o.x = 0;
+    } else if (op == (uint32_t)kOpAcquire) {                                   // :106-108, :119-121
+        o.x = o.cval >= L.max_permits ? (uint64_t)(now + L.cache_ttl_ms) : 0;
+        o.mutate |= o.x != x;
+    }
     return o;
 }
 
@@ -465,8 +500,11 @@ __device__ inline void sw_commit_allows(const DevLimiter& L, const SWGeo& g, uin
 }
 
 // A slot is kept when the region is loaded iff some request at now >= batch_min could
-// still read it; everything else is dropped (the region is rebuilt in LDS).
-__device__ inline bool slot_live(const DevLimiter& L, const Slot& s, int64_t batch_min) {
+// still read it (x: its local-cache block-until, SW with the cache on); everything else is
+// dropped (the region is rebuilt in LDS).
+__device__ inline bool slot_live(const DevLimiter& L, const Slot& s, int64_t batch_min,
+                                 uint64_t x = 0) {
+    if (x != 0 && (int64_t)x > batch_min) return true;
     if (L.algo == kAlgoTB) {
         return (s.c & 1u) && !(batch_min > (int64_t)s.b + L.ttl_ms);
     }

@@ -38,6 +38,7 @@ struct HostLimiter {
     DevLimiter dev;
     void* table = nullptr;
     size_t table_bytes = 0;
+    void* cache_table = nullptr;            // SW local cache: u64 per slot
 };
 
 inline int ceil_log2(uint64_t x) {
@@ -230,7 +231,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
 extern "C" void rl_destroy(rl_engine* e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
-    for (auto& l : e->lims) dfree(l.table);
+    for (auto& l : e->lims) { dfree(l.table); dfree(l.cache_table); }
     dfree(e->d_lims); dfree(e->d_region_lim);
     dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
     dfree(e->ext);
@@ -272,6 +273,7 @@ extern "C" int rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* c, uint1
     std::lock_guard<std::mutex> lk(e->mu);
     // RateLimitConfig.validate() (RateLimitConfig.java:46-56)
     if (c->max_permits <= 0 || c->window_ms <= 0 || !(c->refill_per_s >= 0.0)) return RL_E_INVALID_ARG;
+    if ((c->flags & ~RL_LIM_LOCAL_CACHE) != 0 || c->local_cache_ttl_ms < 0) return RL_E_INVALID_ARG;
     if (c->algo == RL_ALGO_TOKEN_BUCKET && !(c->refill_per_s > 0.0)) return RL_E_INVALID_ARG;  // TB ctor :77-79
     if (c->algo != RL_ALGO_TOKEN_BUCKET && c->algo != RL_ALGO_SLIDING_WINDOW) return RL_E_INVALID_ARG;
     if (c->window_ms > RL_MAX_WINDOW_MS) return RL_E_INVALID_ARG;
@@ -303,6 +305,13 @@ extern "C" int rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* c, uint1
     if (dalloc(&h.table, h.table_bytes) != RL_OK) return RL_E_NOMEM;
     if (hipMemset(h.table, 0, h.table_bytes) != hipSuccess) { dfree(h.table); return RL_E_DEVICE; }
     d.table = (uint64_t)(uintptr_t)h.table;
+    if (c->algo == RL_ALGO_SLIDING_WINDOW && (c->flags & RL_LIM_LOCAL_CACHE) && c->local_cache_ttl_ms > 0) {
+        const size_t xb = (size_t)(1ULL << k) * kRegionSlots * sizeof(uint64_t);
+        if (dalloc(&h.cache_table, xb) != RL_OK) { dfree(h.table); return RL_E_NOMEM; }
+        if (hipMemset(h.cache_table, 0, xb) != hipSuccess) { dfree(h.table); dfree(h.cache_table); return RL_E_DEVICE; }
+        d.cache_table = (uint64_t)(uintptr_t)h.cache_table;
+        d.cache_ttl_ms = c->local_cache_ttl_ms;
+    }
     e->lims.push_back(h);
     e->n_regions += 1u << k;
     int rc = upload_limiters(e);
@@ -318,7 +327,7 @@ extern "C" int rl_add_limiter(rl_engine* e, int algo, int64_t max_permits, int64
     c.max_permits = max_permits;
     c.window_ms = window_ms;
     c.refill_per_s = refill_per_s;
-    c.capacity = 0;
+    c.capacity = 0;                                  // local cache off: the parity-mode default
     return rl_add_limiter_ex(e, &c, id);
 }
 
@@ -414,7 +423,9 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     const int res_bytes = res_bytes_for(max_any, wide);
     const uint32_t nt = (uint32_t)((n + kTile - 1) / kTile);
-    const int bsh = e->bin_shift;
+    bool cache = false;
+    for (auto& l : e->lims) cache |= l.dev.cache_ttl_ms > 0;
+    const int bsh = cache ? 0 : e->bin_shift;        // the local-cache kernel is bin_shift 0
     const uint32_t n_bins = e->n_regions >> bsh;
     const int bitsP = std::max(1, ceil_log2(n_bins));
     const int passes = bitsP <= kMaxDigitBits ? 1 : 2;
@@ -427,7 +438,9 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         rc = ensure_regions(e, n_bins);
         if (rc != RL_OK) return rc;
     }
-    const bool hot = e->hot_threshold > 0 && bsh == 0;
+    // the hot-key path assumes that a denial never changes state; with a local cache a
+    // denial may (it puts the estimate, SlidingWindowRateLimiter.java:106-108)
+    const bool hot = e->hot_threshold > 0 && bsh == 0 && !cache;
     if (hot) {
         rc = ensure_hot_mark(e, n_bins);
         if (rc == RL_OK) rc = ensure_hot_summ(e, n);
@@ -502,6 +515,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
     ra.skew_ms = e->opts.max_skew_ms;
     ra.stats = e->d_stats;
+    ra.cache = cache ? 1u : 0u;
     if (e->debug_regions) {
         if (e->dbg_cap < (size_t)n_bins * kDbgWords) {
             dfree(e->dbg);
@@ -683,6 +697,7 @@ extern "C" int rl_batch_stats_get(rl_engine* e, rl_batch_stats* out) {
     out->capacity_errors = c.cap_err;
     out->regions_touched = c.regions;
     out->table_bytes = c.regions * (uint64_t)kRegionSlots * sizeof(Slot) * 2;
+    out->cache_hits = c.cache_hits;
     return RL_OK;
 }
 

@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
             c->max_now_key = 0;
             c->span_overflow = 0;
             c->n_esc = 0;
-            c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = 0;
+            c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = c->cache_hits = 0;
         }
     }
     const uint32_t mask = bins - 1;
@@ -458,11 +458,18 @@ __device__ inline void wave_fence() { __builtin_amdgcn_wave_barrier(); asm volat
 __device__ inline uint32_t slot_home(uint64_t h) { return (uint32_t)h & (kRegionSlots - 4); }
 
 struct RegionTable {
+    static constexpr bool kCache = false;
     alignas(16) uint64_t tag[kRegionSlots];
     uint64_t sa[kRegionSlots];
     uint64_t sb[kRegionSlots];
     uint64_t sc[kRegionSlots];
     alignas(16) uint32_t occ[kRegionSlots];   // bit0 occupied, bit1 touched by this batch
+};
+// With a sliding-window local cache (SlidingWindowRateLimiter.java:57-64): every slot also
+// carries its key's cache state (block-until ms, sw_step_cache), moved with the slot.
+struct RegionTableX : RegionTable {
+    static constexpr bool kCache = true;
+    uint64_t sx[kRegionSlots];
 };
 
 template <class Codec, bool RING>
@@ -501,9 +508,12 @@ template <class Codec, int ALGO, class LdsT>
 __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimiter& L,
                                      uint32_t lane, const typename Codec::Rec& cur, bool valid,
                                      uint32_t j, int64_t base, uint32_t pad, uint32_t& n_allowed,
-                                     uint32_t& n_invalid, uint32_t& n_caperr, uint32_t& n_rounds) {
+                                     uint32_t& n_invalid, uint32_t& n_caperr, uint32_t& n_rounds,
+                                     uint32_t& n_hits) {
     constexpr uint32_t NS = kRegionSlots;
     constexpr bool tb = ALGO == kAlgoTB;        // per-algorithm code: nothing of the other
+    constexpr bool CACHE = LdsT::kCache && !tb;
+    const bool cache_on = CACHE && L.cache_ttl_ms > 0;
     Applied r;
     r.j = valid ? j : pad;
     const Req q = Codec::dec(cur, base);
@@ -545,6 +555,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         wave_fence();
         if (need && atomicCAS(&S.occ[cand], 0u, 1u) == 0u) {
             S.tag[cand] = q.h; S.sa[cand] = 0; S.sb[cand] = 0; S.sc[cand] = 0;
+            if constexpr (LdsT::kCache) S.sx[cand] = 0;
             slot = (int32_t)cand;
             need = false;
         }
@@ -586,7 +597,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         ++n_rounds;
         Outcome o{};
         SWAllow al{false, 0};
-        bool elig = false;
+        bool elig = false, hit = false;
         const uint64_t pm = __ballot(pending);
         const uint64_t kp = peers & pm;                        // my key's pending requests
         if (pending) {
@@ -597,6 +608,11 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             } else {
                 if constexpr (tb) {
                     o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
+                } else if (cache_on) {
+                    // local cache on: every put may change the cache state, so one state
+                    // change per key per round (hypothesis D only)
+                    if constexpr (CACHE)
+                        o = sw_step_cache(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc, S.sx[slot], hit);
                 } else {
                     o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc);
                     // (A) needs: all pending peers acquires in one window, not before the
@@ -634,11 +650,15 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 }
             }
         } else if (pending && lane <= fm) {
-            if (lane == fm) { S.sa[slot] = o.a; S.sb[slot] = o.b; S.sc[slot] = o.c; }
+            if (lane == fm) {
+                S.sa[slot] = o.a; S.sb[slot] = o.b; S.sc[slot] = o.c;
+                if constexpr (CACHE) if (cache_on) S.sx[slot] = o.x;
+            }
             r.alw = o.allowed;
             r.rem = o.remaining;
             r.tok = o.tokens;
             n_allowed += o.allowed ? 1u : 0u;
+            n_hits += hit ? 1u : 0u;                   // counted once, when final
             pending = false;
         }
         wave_fence();
@@ -658,6 +678,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     const uint32_t n_bins = a.n_regions / RPB;
     if (bin >= n_bins) return;
     if (a.hot_mark && a.hot_mark[bin] == a.epoch) return;     // owned by hot_chain
+    if (a.ablate & kAblNoNormal) return;
     const uint32_t start = a.rstart[bin];
     const uint32_t cnt = a.rend ? a.rend[bin] - start : a.rcount[bin];
     if (cnt == 0) return;
@@ -693,25 +714,31 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     // ---- load the region, dropping entries no request of this batch can see, and
     // rebuild its open-addressing table (no tombstones ever reach HBM)
     Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
+    uint64_t* xtab = nullptr;                       // the slots' local-cache states
+    if constexpr (LdsT::kCache)
+        if (L.cache_table) xtab = (uint64_t*)L.cache_table + (size_t)(region - L.region_base) * NS;
     Slot img[NS / 64];
+    uint64_t xim[NS / 64];
 #pragma unroll
     for (uint32_t i = 0; i < NS / 64; ++i) {
         S.occ[lane + 64 * i] = 0;
         img[i] = tab[lane + 64 * i];
+        xim[i] = xtab ? xtab[lane + 64 * i] : 0;
     }
     wave_fence();
 #pragma unroll
     for (uint32_t i = 0; i < NS / 64; ++i) {
         const Slot v = img[i];
-        if (slot_live(L, v, batch_min)) {
+        if (slot_live(L, v, batch_min, xim[i])) {
             uint32_t p = slot_home(v.tag);
             while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
             S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
+            if constexpr (LdsT::kCache) S.sx[p] = xim[i];
         }
     }
     wave_fence();
 
-    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0;
+    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_hits = 0;
     const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t head = 0, count = 0;                    // ring state (wave-uniform)
     // the whole stream is instantiated once per algorithm (uniform per region), so the
@@ -723,7 +750,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
             if constexpr (RPB == 1) {
                 // the bin is the region: every record is ours, applied straight from registers
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, idx < end, idx, base, pad,
-                                                     n_allowed, n_invalid, n_caperr, n_rounds);
+                                                     n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             } else {
@@ -742,7 +769,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 if (count >= 64) {
                     const uint32_t ri = (head + lane) % kRing;
                     ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
-                                           n_allowed, n_invalid, n_caperr, n_rounds);
+                                           n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
                     head = (head + 64) % kRing;
                     count -= 64;
                 }
@@ -770,7 +797,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 const bool v = lane < count;
                 const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
-                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds);
+                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
@@ -787,12 +814,15 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         if (o & 1u) { v.tag = S.tag[s]; v.a = S.sa[s]; v.b = S.sb[s]; v.c = S.sc[s]; }
         else { v.tag = 0; v.a = 0; v.b = 0; v.c = 0; }
         tab[s] = v;
+        if constexpr (LdsT::kCache)
+            if (xtab) xtab[s] = (o & 1u) ? S.sx[s] : 0;
         touched += (o >> 1) & 1u;
     }
     for (int off = 32; off > 0; off >>= 1) {
         n_allowed += __shfl_xor(n_allowed, off, 64);
         n_invalid += __shfl_xor(n_invalid, off, 64);
         n_caperr += __shfl_xor(n_caperr, off, 64);
+        n_hits += __shfl_xor(n_hits, off, 64);
         touched += __shfl_xor(touched, off, 64);
     }
     if (lane == 0) {
@@ -802,6 +832,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
         atomicAdd(st + kStDistinct, (unsigned long long)touched);
         atomicAdd(st + kStRegions, 1ULL);
+        if (n_hits) atomicAdd(st + kStCacheHits, (unsigned long long)n_hits);
         if (a.dbg) {
             uint64_t* d = a.dbg + (size_t)bin * kDbgWords;
             d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = cnt; d[3] = n_rounds;
@@ -1406,8 +1437,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         auto apply64 = [&](uint32_t valid_n) {
             const bool v = lane < valid_n;
             const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
+            uint32_t n_hits = 0;                          // (no local cache on the hot path)
             const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
-                                                    pad, n_allowed, n_invalid, n_caperr, n_rounds);
+                                                    pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
             if (v) {
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
@@ -1511,9 +1543,12 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 // HOT: 2-wave workgroups; the first kHotMax run the hot regions' chains (hot_chain), the
 // rest two normal regions each: one launch, so the chains are dispatched before the
 // normal regions fill the machine, at the LDS per wave of the plain kernel.
-template <class Codec, class Res, bool TOK, int BS, bool HOT>
+template <class Codec, class Res, bool TOK, int BS, bool HOT, bool CACHE = false>
 __global__ __launch_bounds__(HOT ? 128 : 64, HOT ? 4 : 1) void k_regions(RegionArgs a) {
-    if constexpr (HOT) {
+    if constexpr (CACHE) {                       // some limiter keeps a local cache (BS 0, no hot path)
+        __shared__ RegionTableX S;
+        region_body_t<Codec, Res, TOK, 0>(a, blockIdx.x, S);
+    } else if constexpr (HOT) {
         __shared__ union U { RegionTable two[2]; RegionLds<Codec, true> one; } S;
         if (blockIdx.x < kHotMax) {
             hot_chain<Codec, Res, TOK>(a, blockIdx.x, S.one);
@@ -2246,8 +2281,13 @@ __global__ __launch_bounds__(256) void k_sweep(Slot* __restrict__ tab, uint64_t 
     bool dead = false;
     if (i < n_slots) {
         const Slot v = tab[i];
-        dead = (v.tag | v.a | v.b | v.c) != 0 && !slot_live(L, v, now);
-        if (dead) tab[i] = Slot{0, 0, 0, 0};
+        uint64_t* xt = (uint64_t*)L.cache_table;
+        const uint64_t x = xt ? xt[i] : 0;
+        dead = (v.tag | v.a | v.b | v.c) != 0 && !slot_live(L, v, now, x);
+        if (dead) {
+            tab[i] = Slot{0, 0, 0, 0};
+            if (xt) xt[i] = 0;
+        }
     }
     const uint64_t m = __ballot(dead);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (uint32_t)__popcll(m));
@@ -2338,6 +2378,10 @@ static void region_launch(const RegionArgs& a, hipStream_t s) {
         const dim3 g(kHotMax + (a.n_regions + 1) / 2), b2(128);
         if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0, true>), g, b2, 0, s, a);
         else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0, true>), g, b2, 0, s, a);
+    } else if (a.bin_shift == 0 && a.cache) {
+        const dim3 g(a.n_regions);
+        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0, false, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0, false, true>), g, b, 0, s, a);
     } else if (a.bin_shift == 0) {
         const dim3 g(a.n_regions);
         if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0, false>), g, b, 0, s, a);
@@ -2354,24 +2398,24 @@ static void region_launch(const RegionArgs& a, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_stats_reduce(unsigned long long* stats, BatchCtl* ctl) {
     __shared__ unsigned long long part[kStWords][4];
     const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long acc[kStCount] = {};
     for (uint32_t s = t; s < kStatSlots; s += 256) {
         unsigned long long* p = stats + (size_t)s * kStWords;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) { acc[k] += p[k]; p[k] = 0; }
+        for (int k = 0; k < (int)kStCount; ++k) { acc[k] += p[k]; p[k] = 0; }
     }
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < (int)kStCount; ++k) {
         unsigned long long v = acc[k];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
         if (lane == 0) part[k][wid] = v;
     }
     __syncthreads();
-    if (t < 5) {
+    if (t < kStCount) {
         const unsigned long long v = part[t][0] + part[t][1] + part[t][2] + part[t][3];
         unsigned long long* dst = t == kStAllowed ? &ctl->allowed : t == kStInvalid ? &ctl->invalid
                                 : t == kStCapErr ? &ctl->cap_err : t == kStDistinct ? &ctl->distinct
-                                : &ctl->regions;
+                                : t == kStRegions ? &ctl->regions : &ctl->cache_hits;
         *dst += v;
     }
 }

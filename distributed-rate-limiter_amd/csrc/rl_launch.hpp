@@ -17,6 +17,7 @@ enum : uint32_t {
     kAblNoStep = 1u << 8,        // region: skip the per-request semantics
     kAblNoProbe = 1u << 9,       // region: slot = home (no lookup / insert)
     kAblNoRounds = 1u << 10,     // region: one round, no peer match
+    kAblNoNormal = 1u << 11,     // region: skip every non-hot region (hot chains run alone)
     kAblNoGather = 1u << 16,     // unpermute: skip the res gather
 };
 
@@ -32,6 +33,7 @@ struct BatchCtl {
     unsigned long long invalid;
     unsigned long long cap_err;
     unsigned long long regions;
+    unsigned long long cache_hits; // SW local-cache rejections (ratelimiter.cache.hits)
 };
 
 struct PartArgs {
@@ -81,6 +83,7 @@ struct RegionArgs {
     uint32_t ablate;
     int64_t skew_ms;           // rl_opts.max_skew_ms: slots kept until dead at batch min - skew
     unsigned long long* stats; // [kStatSlots][8] sharded batch counters (k_stats_reduce)
+    uint32_t cache;            // some limiter keeps a local cache (k_regions<..., CACHE>)
     const uint32_t* rend;      // nullable: bin b holds records [rstart[b], rend[b]) (2 passes)
     // hot regions (bin_shift 0): k_hot_select lists the largest bins (>= hot_threshold
     // records, at most kHotMax); the k_hot_* kernels own them (hot_mark[bin] == epoch),
@@ -106,7 +109,8 @@ constexpr uint32_t kDbgWords = 8;        // debug words per bin
 // 1.3M-region batch on ONE set of words serialises for >10 ms. Region waves add to slot
 // (block id mod kStatSlots), one 64-B line per slot; k_stats_reduce folds them into BatchCtl.
 constexpr uint32_t kStatSlots = 1024;
-enum : uint32_t { kStAllowed = 0, kStInvalid, kStCapErr, kStDistinct, kStRegions, kStWords = 8 };
+enum : uint32_t { kStAllowed = 0, kStInvalid, kStCapErr, kStDistinct, kStRegions, kStCacheHits,
+                  kStCount, kStWords = 8 };
 
 struct HotInfo {             // one listed hot region
     uint64_t tag;            // its dominant key (mix64 of the key hash)

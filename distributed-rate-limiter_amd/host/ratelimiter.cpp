@@ -43,12 +43,26 @@ uint16_t GpuEngine::addLimiter(int algo, const RateLimitConfig& c) {
     lc.window_ms = c.windowMs;
     lc.refill_per_s = c.refillRate;
     lc.capacity = c.expectedKeys;
+    if (algo == RL_ALGO_SLIDING_WINDOW && c.enableLocalCache && c.localCacheTtlMs > 0) {
+        lc.flags = RL_LIM_LOCAL_CACHE;               // SlidingWindowRateLimiter.java:57-64
+        lc.local_cache_ttl_ms = c.localCacheTtlMs;
+    }
     uint16_t id = 0;
     int st = rl_add_limiter_ex(e_, &lc, &id);
     if (st == RL_E_INVALID_ARG)
         throw IllegalArgumentException(std::string("limiter configuration rejected: ") + rl_strerror(st));
     if (st != RL_OK) throw StorageException(std::string("rl_add_limiter: ") + rl_strerror(st), st);
     return id;
+}
+
+int GpuEngine::executeBatch(size_t n, const uint64_t* key, const int32_t* permits,
+                            const int64_t* now, const uint16_t* limiter, const uint8_t* op,
+                            uint8_t* allowed, int64_t* remaining, uint64_t* cacheHits) {
+    std::lock_guard<std::mutex> lk(mu_);
+    const int st = rl_execute_batch(e_, n, key, permits, now, limiter, op, allowed, remaining, nullptr);
+    rl_batch_stats bs{};
+    if (cacheHits) *cacheHits = rl_batch_stats_get(e_, &bs) == RL_OK ? bs.cache_hits : 0;
+    return st;
 }
 
 GpuRateLimiter::GpuRateLimiter(std::shared_ptr<GpuEngine> engine, Algorithm algo,
@@ -116,8 +130,10 @@ void GpuRateLimiter::flushLocked(std::unique_lock<std::mutex>& lk) {
     for (size_t i = 0; i < n; ++i) {
         k[i] = batch[i]->key; pm[i] = batch[i]->permits; t[i] = batch[i]->now; op[i] = batch[i]->op;
     }
-    int st = rl_execute_batch(engine_->handle(), n, k.data(), pm.data(), t.data(), lim.data(),
-                              op.data(), al.data(), rem.data(), nullptr);
+    uint64_t hits = 0;
+    int st = engine_->executeBatch(n, k.data(), pm.data(), t.data(), lim.data(), op.data(), al.data(),
+                                   rem.data(), &hits);
+    cacheHits.increment(hits);
     lk.lock();
     for (size_t i = 0; i < n; ++i) {
         batch[i]->allowed = al[i];
@@ -161,8 +177,10 @@ void GpuRateLimiter::tryAcquireBatch(size_t n, const uint64_t* keyHash, const in
         cv_.wait(lk, [&] { return !flushing_; });
         flushing_ = true;
         lk.unlock();
-        st = rl_try_acquire_batch(engine_->handle(), n, keyHash, permits, nowNanos, lim.data(),
-                                  al.data(), rem.data(), nullptr);
+        uint64_t hits = 0;
+        st = engine_->executeBatch(n, keyHash, permits, nowNanos, lim.data(), nullptr, al.data(),
+                                   rem.data(), &hits);
+        cacheHits.increment(hits);
         lk.lock();
         flushing_ = false;
         cv_.notify_all();

@@ -111,9 +111,15 @@ class GpuEngine {
     GpuEngine& operator=(const GpuEngine&) = delete;
     rl_engine* handle() const { return e_; }
     uint16_t addLimiter(int algo, const RateLimitConfig& c);
+    // Runs one host batch and returns its status and cache-hit count atomically with
+    // respect to the other limiters sharing this engine.
+    int executeBatch(size_t n, const uint64_t* key, const int32_t* permits, const int64_t* now,
+                     const uint16_t* limiter, const uint8_t* op, uint8_t* allowed,
+                     int64_t* remaining, uint64_t* cacheHits);
 
   private:
     rl_engine* e_ = nullptr;
+    std::mutex mu_;
 };
 
 // Clock in nanoseconds (the reference reads System.currentTimeMillis(); injectable so a
@@ -146,6 +152,7 @@ class GpuRateLimiter : public RateLimiter {
     const RateLimitConfig& config() const { return cfg_; }
     Counter allowedRequests;
     Counter rejectedRequests;
+    Counter cacheHits{"ratelimiter.cache.hits"};     // SlidingWindowRateLimiter.java:75-77
 
   private:
     struct Pending {

@@ -66,16 +66,20 @@ class Opts(ctypes.Structure):
                 ("max_skew_ms", ctypes.c_int64)]
 
 
+LIM_LOCAL_CACHE = 1
+
+
 class LimiterConfig(ctypes.Structure):
-    _fields_ = [("algo", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    _fields_ = [("algo", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("max_permits", ctypes.c_int64), ("window_ms", ctypes.c_int64),
-                ("refill_per_s", ctypes.c_double), ("capacity", ctypes.c_uint64)]
+                ("refill_per_s", ctypes.c_double), ("capacity", ctypes.c_uint64),
+                ("local_cache_ttl_ms", ctypes.c_int64)]
 
 
 class BatchStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("n", "allowed", "distinct_keys", "invalid",
                                                  "capacity_errors", "regions_touched",
-                                                 "table_bytes")]
+                                                 "table_bytes", "cache_hits")]
 
 
 class TraceSpec(ctypes.Structure):
@@ -239,10 +243,14 @@ class Engine:
     def handle(self):
         return self._h
 
-    def add_limiter(self, algo, max_permits, window_ms, refill_per_s=0.0, capacity=0) -> int:
-        c = LimiterConfig(algo=int(algo), reserved=0, max_permits=int(max_permits),
-                          window_ms=int(window_ms), refill_per_s=float(refill_per_s),
-                          capacity=int(capacity))
+    def add_limiter(self, algo, max_permits, window_ms, refill_per_s=0.0, capacity=0,
+                    local_cache_ttl_ms=0) -> int:
+        """local_cache_ttl_ms > 0: the sliding window's Caffeine local cache (parity mode,
+        the default, has it off as the reference's own test does)."""
+        c = LimiterConfig(algo=int(algo), flags=LIM_LOCAL_CACHE if local_cache_ttl_ms else 0,
+                          max_permits=int(max_permits), window_ms=int(window_ms),
+                          refill_per_s=float(refill_per_s), capacity=int(capacity),
+                          local_cache_ttl_ms=int(local_cache_ttl_ms))
         lid = ctypes.c_uint16()
         st = self._L.rl_add_limiter_ex(self._h, ctypes.byref(c), ctypes.byref(lid))
         if st != RL_OK:

@@ -101,13 +101,22 @@ typedef struct rl_opts {
 
 #define RL_OPT_STAGE_TIMING 0x1u  /* record hipEvents around every stage (rl_stage_times) */
 
+#define RL_LIM_LOCAL_CACHE 0x1u  /* RateLimitConfig.enableLocalCache (RateLimitConfig.java:37-38) */
+
 typedef struct rl_limiter_config {
     int32_t  algo;              /* RL_ALGO_*                                                  */
-    int32_t  reserved;
+    uint32_t flags;             /* RL_LIM_* bits                                              */
     int64_t  max_permits;       /* RateLimitConfig.maxPermits (RateLimitConfig.java:19)       */
     int64_t  window_ms;         /* RateLimitConfig.window.toMillis() (RateLimitConfig.java:24) */
     double   refill_per_s;      /* RateLimitConfig.refillRate (RateLimitConfig.java:31); TB only */
     uint64_t capacity;          /* expected live keys (table sizing); 0 = rl_opts.default_capacity */
+    int64_t  local_cache_ttl_ms;/* RateLimitConfig.localCacheTtl (RateLimitConfig.java:43-44);
+                                   with RL_LIM_LOCAL_CACHE on a sliding window the engine
+                                   emulates SlidingWindowRateLimiter's Caffeine cache
+                                   (:57-64,93-121,148-150) deterministically in trace time:
+                                   expireAfterWrite(ttl) at ms resolution, no size eviction
+                                   (exact while <= 10k keys are cached, maximumSize(10000)).
+                                   Token buckets have no cache (TokenBucketRateLimiter). */
 } rl_limiter_config;
 
 typedef struct rl_batch_stats {
@@ -118,6 +127,8 @@ typedef struct rl_batch_stats {
     uint64_t capacity_errors;   /* requests not applied because a region was full            */
     uint64_t regions_touched;   /* state-table regions loaded + written back                  */
     uint64_t table_bytes;       /* bytes of state-table regions moved (load + write-back)     */
+    uint64_t cache_hits;        /* SW local-cache rejections (ratelimiter.cache.hits,
+                                   SlidingWindowRateLimiter.java:75-77,96)                  */
 } rl_batch_stats;
 
 /* Create / destroy an engine on one GPU. Replaces the JedisPool + Redis keyspace

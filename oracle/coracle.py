@@ -44,6 +44,9 @@ def lib():
         L.orc_run_sharded.restype = ctypes.c_size_t
         L.orc_live_keys.argtypes = [vp]
         L.orc_live_keys.restype = ctypes.c_size_t
+        L.orc_set_local_cache.argtypes = [vp, ctypes.c_int, ctypes.c_int64]
+        L.orc_cache_hits.argtypes = [vp]
+        L.orc_cache_hits.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -63,14 +66,21 @@ class COracle:
         for spec in limiters:
             self.add_limiter(*spec)
 
-    def add_limiter(self, algo, max_permits, window_ms, refill_per_s=0.0) -> int:
+    def add_limiter(self, algo, max_permits, window_ms, refill_per_s=0.0, capacity=0,
+                    local_cache_ttl_ms=0) -> int:
         ids = {self._L.orc_add_limiter(s, int(algo), int(max_permits), int(window_ms),
                                        float(refill_per_s)) for s in self._states}
         (lid,) = ids
         if lid < 0:
             raise ValueError("invalid limiter config (RateLimitConfig.validate)")
+        if local_cache_ttl_ms:
+            for s in self._states:
+                self._L.orc_set_local_cache(s, lid, int(local_cache_ttl_ms))
         self.n_limiters += 1
         return lid
+
+    def cache_hits(self) -> int:
+        return sum(self._L.orc_cache_hits(s) for s in self._states)
 
     def run(self, keys, permits, now_ns, limiter=None, ops=None, want_tokens=True):
         keys = np.ascontiguousarray(keys, dtype=np.uint64)

@@ -12,6 +12,11 @@
  *     tryAcquire (:105-143) and the embedded Lua script (:38-68)
  *   - RedisRateLimitStorage.incrementAndExpire / get / evalScript
  *       (storage/RedisRateLimitStorage.java:38-59,133-139)
+ *   - the Caffeine local cache of SlidingWindowRateLimiter when enabled (:57-64,93-100,
+ *     106-108,119-121,148-150). Caffeine 3.1.8 (pom.xml:23, not vendored) restated from its
+ *     published behaviour: expireAfterWrite(ttl) returns an entry written at w iff
+ *     now - w < ttl; put overwrites value and write time; maximumSize(10000) eviction
+ *     (W-TinyLFU, non-deterministic) is not modelled (exact while <= 10k keys are cached)
  *   - Redis 7 keyspace semantics the above rely on (not vendored; restated from the
  *     published behaviour): INCR on a missing/expired key creates it with 1; PEXPIRE
  *     sets expireAt = now + ttl; a key is expired (reads as missing) iff now > expireAt;
@@ -56,9 +61,11 @@ typedef struct {
     int64_t window_ms;
     double refill_rate;     /* permits per second (RateLimitConfig.refillRate) */
     double rate_per_ms;     /* TokenBucketRateLimiter.java:85 */
+    int64_t cache_ttl;      /* SW local cache expireAfterWrite, ms (0: no cache) */
 } orc_limiter;
 
-/* One Redis key. ns: 1 = "rl:" counter, 2 = "tb:" hash. */
+/* One Redis key. ns: 1 = "rl:" counter, 2 = "tb:" hash, 3 = a Caffeine cache entry
+ * (counter = cached value, aux = write time; not a Redis key). */
 typedef struct {
     uint8_t used;           /* slot holds a key (possibly logically deleted) */
     uint8_t present;        /* key exists (not deleted) */
@@ -70,6 +77,7 @@ typedef struct {
     double tokens;          /* HMSET field tokens ("tb") */
     double last_refill;     /* HMSET field last_refill ("tb") */
     int64_t expire_at;      /* PEXPIRE: now + ttl; INT64_MAX = persistent */
+    int64_t aux;            /* cache entry write time (ns 3) */
 } orc_entry;
 
 typedef struct {
@@ -82,6 +90,7 @@ typedef struct orc_state {
     orc_limiter lim[ORC_MAX_LIMITERS];
     int n_lim;
     orc_keyspace ks;
+    uint64_t cache_hits;    /* ratelimiter.cache.hits (SlidingWindowRateLimiter.java:75-77) */
 } orc_state;
 
 /* ---------------- keyspace (hash map) ---------------- */
@@ -218,17 +227,43 @@ static int64_t sw_incr_expire(orc_state* s, uint16_t lim, uint64_t key, int64_t 
     return e->counter;
 }
 
-/* tryAcquire(key, permits) (:85-131), local cache disabled (parity mode). */
+/* Caffeine getIfPresent / put (expireAfterWrite). */
+static int cache_get(orc_state* s, uint16_t lim, uint64_t key, int64_t now, int64_t* value) {
+    orc_entry* e = ks_find_slot(&s->ks, 3, lim, key, 0);
+    if (!e->used || !e->present) return 0;
+    if (!(now - e->aux < s->lim[lim].cache_ttl)) return 0;
+    *value = e->counter;
+    return 1;
+}
+
+static void cache_put(orc_state* s, uint16_t lim, uint64_t key, int64_t value, int64_t now) {
+    orc_entry* e = ks_find_slot(&s->ks, 3, lim, key, 0);
+    if (!e->used || !e->present) e = ks_create(&s->ks, 3, lim, key, 0);
+    e->counter = value;
+    e->aux = now;
+}
+
+/* tryAcquire(key, permits) (:85-131), with the local cache when the limiter enables it. */
 static void sw_try_acquire(orc_state* s, uint16_t lim, uint64_t key, int32_t permits,
                            int64_t now, uint8_t* allowed, int64_t* remaining) {
     const orc_limiter* L = &s->lim[lim];
+    int64_t cached;
+    if (L->cache_ttl > 0 && cache_get(s, lim, key, now, &cached) && cached >= L->max_permits) {
+        s->cache_hits++;                             /* :93-100: rejected, no Redis access */
+        *allowed = 0;
+        int64_t r = L->max_permits - sw_current_count(s, lim, key, now);
+        *remaining = r > 0 ? r : 0;
+        return;
+    }
     int64_t currentCount = sw_current_count(s, lim, key, now);
     if (currentCount + (int64_t)permits > L->max_permits) {
         *allowed = 0;
+        if (L->cache_ttl > 0) cache_put(s, lim, key, currentCount, now);      /* :106-108 */
     } else {
         int64_t windowMs = L->window_ms;
         int64_t currentKeyStart = sw_window_start(now, windowMs);
         int64_t newCount = sw_incr_expire(s, lim, key, currentKeyStart, now, windowMs);
+        if (L->cache_ttl > 0) cache_put(s, lim, key, newCount, now);          /* :119-121 */
         *allowed = (uint8_t)(newCount <= L->max_permits);
     }
     /* batch convention: getAvailablePermits at the same now, after */
@@ -247,6 +282,7 @@ static void sw_reset(orc_state* s, uint16_t lim, uint64_t key, int64_t now) {
     int64_t windowMs = s->lim[lim].window_ms;            /* :139-153 */
     ks_delete(&s->ks, 1, lim, key, sw_window_start(now, windowMs));
     ks_delete(&s->ks, 1, lim, key, sw_window_start(now - windowMs, windowMs));
+    ks_delete(&s->ks, 3, lim, key, 0);                   /* :148-150 localCache.invalidate */
 }
 
 /* ---------------- TokenBucketRateLimiter + Lua ---------------- */
@@ -357,8 +393,19 @@ int orc_add_limiter(orc_state* s, int algo, int64_t max_permits, int64_t window_
     L->window_ms = window_ms;
     L->refill_rate = refill_per_s;
     L->rate_per_ms = refill_per_s / 1000.0;
+    L->cache_ttl = 0;
     return s->n_lim++;
 }
+
+/* Enable the SW local cache of limiter lid (RateLimitConfig.enableLocalCache /
+ * localCacheTtl, RateLimitConfig.java:37-44). TB limiters have no cache. */
+int orc_set_local_cache(orc_state* s, int lid, int64_t ttl_ms) {
+    if (lid < 0 || lid >= s->n_lim || ttl_ms < 0) return -1;
+    s->lim[lid].cache_ttl = s->lim[lid].algo == ORC_SW ? ttl_ms : 0;
+    return 0;
+}
+
+uint64_t orc_cache_hits(orc_state* s) { return s->cache_hits; }
 
 /* Apply one request. Returns 1 if the request was invalid. */
 static int orc_one(orc_state* s, uint64_t key, int32_t permits, int64_t now_ns, uint16_t lim,
@@ -453,6 +500,7 @@ size_t orc_run_sharded(orc_state** states, int nthreads, size_t n, const uint64_
 
 size_t orc_live_keys(orc_state* s) {
     size_t c = 0;
-    for (size_t i = 0; i < s->ks.cap; i++) c += s->ks.slots[i].used && s->ks.slots[i].present;
+    for (size_t i = 0; i < s->ks.cap; i++)
+        c += s->ks.slots[i].used && s->ks.slots[i].present && s->ks.slots[i].ns != 3;
     return c;
 }

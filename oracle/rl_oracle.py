@@ -16,6 +16,14 @@ Reference lines restated:
   TokenBucketRateLimiter.java:38-68     (Lua), :85 (ratePerMs), :105-158
   RedisRateLimitStorage.java:38-59      (incrementAndExpire, get), :133-139 (eval)
   RateLimitConfig.java:46-56            (validate)
+  SlidingWindowRateLimiter.java:57-64,93-100,106-108,119-121,148-150
+                                        (the Caffeine local cache, when enabled)
+
+The Caffeine 3.1.8 cache (pom.xml:23; not vendored) is restated from its published
+behaviour: `expireAfterWrite(ttl)` — an entry written at time w is returned by
+getIfPresent at time t iff t - w < ttl — and `put` overwrites value and write time. The
+trace clock is the request's now at ms resolution. `maximumSize(10000)` eviction
+(W-TinyLFU, non-deterministic) is not modelled: exact while at most 10k keys are cached.
 """
 from __future__ import annotations
 
@@ -103,7 +111,7 @@ class Redis:
 
 class Limiter:
     def __init__(self, lid: int, algo: int, max_permits: int, window_ms: int,
-                 refill_per_s: float):
+                 refill_per_s: float, local_cache_ttl_ms: int = 0):
         # RateLimitConfig.validate (RateLimitConfig.java:46-56)
         if max_permits <= 0:
             raise ValueError("maxPermits must be positive")
@@ -117,17 +125,32 @@ class Limiter:
         self.max_permits, self.window_ms = max_permits, window_ms
         self.refill_rate = refill_per_s
         self.rate_per_ms = refill_per_s / 1000.0  # TokenBucketRateLimiter.java:85
+        # SW local cache (SlidingWindowRateLimiter.java:57-64); TB has none
+        self.cache_ttl = int(local_cache_ttl_ms) if algo == SW else 0
 
 
 class PyOracle:
     def __init__(self):
         self.redis = Redis()
         self.limiters: list[Limiter] = []
+        self.cache: dict[tuple, tuple] = {}     # (lid, key) -> (value, write_ms)
+        self.cache_hits = 0                     # ratelimiter.cache.hits (:75-77)
 
-    def add_limiter(self, algo, max_permits, window_ms, refill_per_s=0.0) -> int:
+    def add_limiter(self, algo, max_permits, window_ms, refill_per_s=0.0, capacity=0,
+                    local_cache_ttl_ms=0) -> int:
         self.limiters.append(Limiter(len(self.limiters), algo, max_permits, window_ms,
-                                     refill_per_s))
+                                     refill_per_s, local_cache_ttl_ms))
         return len(self.limiters) - 1
+
+    # ---- Caffeine local cache (expireAfterWrite) ----
+    def _cache_get(self, L: Limiter, key, now):
+        e = self.cache.get((L.lid, key))
+        if e is None or not (now - e[1] < L.cache_ttl):
+            return None
+        return e[0]
+
+    def _cache_put(self, L: Limiter, key, value, now):
+        self.cache[(L.lid, key)] = (value, now)
 
     # ---- sliding window ----
     @staticmethod
@@ -144,12 +167,21 @@ class PyOracle:
         return java_d2l(float(prev) * prev_weight + float(curr))
 
     def _sw_acquire(self, L: Limiter, key, permits, now):
+        if L.cache_ttl:                                   # :93-100
+            cached = self._cache_get(L, key, now)
+            if cached is not None and cached >= L.max_permits:
+                self.cache_hits += 1
+                return 0, max(0, L.max_permits - self._current_count(L, key, now))
         cc = self._current_count(L, key, now)
         if cc + permits > L.max_permits:
             allowed = 0
+            if L.cache_ttl:                               # :106-108
+                self._cache_put(L, key, cc, now)
         else:
             nc = self.redis.incr_pexpire(self._window_key(L.lid, key, now, L.window_ms),
                                          L.window_ms, now)
+            if L.cache_ttl:                               # :119-121
+                self._cache_put(L, key, nc, now)
             allowed = int(nc <= L.max_permits)
         return allowed, max(0, L.max_permits - self._current_count(L, key, now))
 
@@ -246,6 +278,7 @@ class PyOracle:
                     w = L.window_ms
                     self.redis.delete(self._window_key(L.lid, key, now, w))
                     self.redis.delete(self._window_key(L.lid, key, now - w, w))
+                    self.cache.pop((L.lid, key), None)    # :148-150 invalidate
                 else:  # TokenBucketRateLimiter.reset :153-158
                     self.redis.delete(f"{L.lid}|tb:{key}")
         return allowed, remaining, tokens

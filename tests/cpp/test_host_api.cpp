@@ -80,6 +80,20 @@ static void gpu_tests() {
     CHECK(sw.allowedRequests.count() == 10 && sw.rejectedRequests.count() == 1);
     CHECK(sw.allowedRequests.name == "ratelimiter.requests.allowed");
 
+    // local cache on (SlidingWindowRateLimiter.java:57-64,93-100): once a put caches a count
+    // >= maxPermits, requests within the TTL are rejected from the cache and counted
+    {
+        RateLimitConfig cc = cfg;
+        cc.enableLocalCache = true;
+        cc.localCacheTtlMs = 100;
+        GpuRateLimiter swc(eng, GpuRateLimiter::Algorithm::SlidingWindow, cc, clk);
+        for (int i = 0; i < 10; ++i) CHECK(swc.tryAcquire("cached_user"));
+        for (int i = 0; i < 5; ++i) CHECK(!swc.tryAcquire("cached_user"));
+        CHECK(swc.cacheHits.count() == 5 && swc.cacheHits.name == "ratelimiter.cache.hits");
+        CHECK(swc.rejectedRequests.count() == 5);
+        CHECK(swc.getAvailablePermits("cached_user") == 0);
+    }
+
     // shouldHandleConcurrentRequests (:134-176): 20 threads x 10 requests on one key with a
     // pinned clock -> exactly maxPermits succeed through the micro-batcher.
     GpuRateLimiter sw2(eng, GpuRateLimiter::Algorithm::SlidingWindow, cfg, clk, 200);
@@ -186,6 +200,7 @@ static void config1() {
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
     CHECK(ok.load() == 100000);
     CHECK(sw.allowedRequests.count() == 100000 && sw.rejectedRequests.count() == 0);
+    CHECK(sw.cacheHits.count() == 0);       // the limit is never reached: no short-circuit
     CHECK(sw.getAvailablePermits("user123") == 0);
     std::printf("config1: 100000 of 100000 allowed, %.3f s, %.0f req/s "
                 "(10 threads, micro-batched; reference published 80,192 req/s)\n", sec, 1e5 / sec);

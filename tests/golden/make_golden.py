@@ -329,6 +329,62 @@ def kats():
         " below zero; nothing is persisted on deny (:66-67), so T0+100 refills from 0.",
         TBL, reqs, exp))
 
+    # ---------- the SW local cache (Caffeine, expireAfterWrite 100 ms) ----------
+    LC = [[SW, 10, 1000, 0.0, 0, 100]]   # [algo, max, w, refill, capacity, localCacheTtl ms]
+    reqs = [req(80, 1, W + 10) for _ in range(10)]
+    reqs += [req(80, 1, W + 50), req(80, 1, W + 109), req(80, 1, W + 110), req(80, 1, W + 209)]
+    # 10 allows; the 10th puts newCount 10 >= max at W+10. W+50, W+109: getIfPresent hits
+    # (age 40, 99 < 100) -> rejected without Redis, remaining = 10 - est(10) = 0. W+110: age
+    # 100 -> expired -> est 10 -> deny, put 10 at W+110. W+209: age 99 -> hit again.
+    exp = [[1, 9 - i, None] for i in range(10)] + [[0, 0, None]] * 4
+    out.append(case(
+        "ref:cache:rejectFromCache",
+        "SlidingWindowRateLimiter.java:93-100: a cached count >= maxPermits rejects without a"
+        " Redis read; put on allow (:119-121) and on deny (:106-108); expireAfterWrite(100 ms)"
+        " (:57-64) returns an entry iff its age < 100 ms.",
+        LC, reqs, exp))
+
+    reqs = [req(81, 1, W + 900) for _ in range(10)]
+    reqs += [req(81, 1, W + 999), req(81, 1, W + 1000), req(81, 1, W + 1050),
+             req(81, 1, W + 1100), req(81, 1, W + 1101)]
+    # W+900 x10 -> allows, put 10 at W+900. W+999: hit -> deny 0. W+1000 (new window): age
+    # 100 -> expired; prev = 10 (alive to W+1900), pw 1.0 -> est 10 -> deny, put 10 at W+1000.
+    # W+1050: hit (age 50) -> deny although Redis alone would allow: est = trunc(10 * 0.95) =
+    # 9 -> remaining 1. W+1100: age 100 -> expired; est = trunc(10 * 0.9) = 9 -> allow, INCR
+    # -> 1, put 1; after: trunc(9.0 + 1) = 10 -> 0. W+1101: pw 0.899, 8.99 + 1 -> 9 -> allow,
+    # after trunc(8.99 + 2) = 10 -> 0.
+    exp = [[1, 9 - i, None] for i in range(10)]
+    exp += [[0, 0, None], [0, 0, None], [0, 1, None], [1, 0, None], [1, 0, None]]
+    out.append(case(
+        "hand:cache:outlivesWindowRollover",
+        "the cache is keyed by the raw key (SlidingWindowRateLimiter.java:94), not by window,"
+        " so a cached rejection outlives the window rollover for up to its TTL: at W+1050 the"
+        " weighted estimate (9) would admit the request, the cached count (10) rejects it.",
+        LC, reqs, exp))
+
+    reqs = [req(82, 1, W + 10) for _ in range(9)]
+    reqs += [req(82, 2, W + 20), req(82, 1, W + 30), req(82, 1, W + 40), req(82, 0, W + 45, op=1)]
+    # 9 allows (remaining 9..1). W+20, permits 2: est 9 + 2 > 10 -> deny, put 9 (< max: no
+    # short-circuit later). W+30: cached 9 < 10 -> Redis path, est 9 -> allow, put 10. W+40:
+    # hit -> deny 0. The peek (getAvailablePermits :133-137) never consults the cache: 0.
+    exp = [[1, 9 - i, None] for i in range(9)]
+    exp += [[0, 1, None], [1, 0, None], [0, 0, None], [0, 0, None]]
+    out.append(case(
+        "hand:cache:putBelowMaxDoesNotReject",
+        "a deny caches the estimate (:106-108); only a cached value >= maxPermits"
+        " short-circuits (:95), so a permits-2 denial at est 9 leaves the next permits-1"
+        " request to Redis.",
+        LC, reqs, exp))
+
+    reqs = [req(83, 1, W + 10) for _ in range(10)]
+    reqs += [req(83, 1, W + 15), req(83, 0, W + 20, op=2), req(83, 1, W + 30)]
+    exp = [[1, 9 - i, None] for i in range(10)] + [[0, 0, None], [0, 0, None], [1, 9, None]]
+    out.append(case(
+        "hand:cache:resetInvalidates",
+        "reset deletes both buckets and invalidates the cached count"
+        " (SlidingWindowRateLimiter.java:139-153): the next request is admitted at once.",
+        LC, reqs, exp))
+
     # ---------- documented outputs of the reference (README / API_EXAMPLES) ----------
     API = [[SW, 100, 60000, 0.0]]     # apiRateLimiter, RateLimiterConfig.java:51-56
     AUTH = [[SW, 10, 60000, 0.0]]     # authRateLimiter, RateLimiterConfig.java:70-74

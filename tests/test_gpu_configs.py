@@ -116,7 +116,8 @@ def config1_trace():
 
 
 def test_config1_single_key_stream():
-    lims = [[rl_amd.SW, 100_000, 60_000, 0.0]]
+    # RateLimiterBenchmark.java:50-55: enableLocalCache(true), localCacheTtl 50 ms
+    lims = [[rl_amd.SW, 100_000, 60_000, 0.0, 0, 50]]
     keys, permits, now = config1_trace()
     want = COracle(lims).run(keys, permits, now, want_tokens=False)
     assert want[0].sum() == 100_000 and want[1][-1] == 0     # README.md:179: 100% success
@@ -130,3 +131,4 @@ def test_config1_single_key_stream():
             got[0].append(a); got[1].append(r)
         assert_same((np.concatenate(got[0]), np.concatenate(got[1]), None), want[:3],
                     f"config1 x{batches}")
+        assert e.stats()["cache_hits"] == 0

@@ -315,3 +315,29 @@ def test_sw_same_key_runs_in_groups(maxp, window):
     op = np.where(rng.random(n) < 0.01, 1, 0).astype(np.uint8)
     got, want, _ = run_both(lims, (keys, permits, now, np.zeros(n, np.uint16), op), batches=3)
     assert_same(got, want, "sw runs")
+
+
+@pytest.mark.parametrize("ttl", [1, 50, 700])
+def test_sw_local_cache_random(ttl):
+    """SlidingWindowRateLimiter's Caffeine cache (:57-64,93-121,148-150) emulated on the GPU:
+    few hot keys at their limits (cache hits, rollovers), peeks and resets, several batches,
+    a cache-less SW limiter and a TB limiter (no cache, TokenBucketRateLimiter) beside it."""
+    lims = [[rl_amd.SW, 10, 1000, 0.0, 0, ttl], [rl_amd.SW, 40, 5000, 0.0],
+            [rl_amd.TB, 20, 1000, 5.0, 0, ttl], [rl_amd.SW, 3, 200, 0.0, 0, ttl]]
+    tr = trace(100 + ttl, 300_000, 2_000, len(lims), 60_000, zipf=1.2, permits_max=3,
+               ops=0.02)
+    got, want, e = run_both(lims, tr, batches=4)
+    assert_same(got, want, f"local cache ttl={ttl}")
+    o = COracle(lims)
+    o.run(*tr)
+    hits = o.cache_hits()
+    assert hits > 0
+    # the engine's counter covers the last batch only: replay the last batch's share
+    e2 = engine(lims)
+    n = len(tr[0])
+    cuts = np.linspace(0, n, 5).astype(int)
+    tot = 0
+    for b in range(4):
+        e2.execute(*(x[cuts[b]:cuts[b + 1]] for x in tr))
+        tot += e2.stats()["cache_hits"]
+    assert tot == hits
