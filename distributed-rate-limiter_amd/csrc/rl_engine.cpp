@@ -110,6 +110,8 @@ struct rl_engine {
     uint32_t* route_scratch = nullptr;
     size_t route_cap = 0;
     uint32_t* route_counts = nullptr;
+    DirSlot* d_dir = nullptr;               // hot-key owner directory (nullptr: hash owners)
+    std::vector<DirSlot> h_dir;             // host copy (rl_owner_of_engine)
 
     hipEvent_t ev[kEvRing][kMarks] = {};
     int ring_used = 0;                      // batches recorded since the last query
@@ -122,6 +124,7 @@ struct rl_engine {
     uint32_t ablate = 0;                    // rl_tune("ablate"), measurement only
     int bin_shift = 0;                      // rl_tune("bin_shift"): 0 or 3 (regions per bin 1/8)
     uint32_t up_per_cu = 0, sc_per_cu = 0, un_per_cu = 0;   // rl_tune("*_per_cu"), 0 = default
+    bool force_wide = false;                // rl_tune("wide_records"): 32-B records (any time span)
 };
 
 #define HIP_OK(x)                                                      \
@@ -241,7 +244,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->d_ctl); dfree(e->d_stats);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
-    dfree(e->route_scratch); dfree(e->route_counts);
+    dfree(e->route_scratch); dfree(e->route_counts); dfree(e->d_dir);
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
     for (int r = 0; r < kEvRing; ++r)
         for (int i = 0; i < kMarks; ++i) if (e->ev[r][i]) (void)hipEventDestroy(e->ev[r][i]);
@@ -415,7 +418,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         e->last_status = RL_E_INVALID_REQUEST;
         return RL_OK;
     }
-    bool wide = false;
+    bool wide = e->force_wide;
     int64_t max_any = 0;
     for (auto& l : e->lims) {
         wide |= l.cfg.max_permits > kCompactMaxPermits;
@@ -645,10 +648,23 @@ extern "C" int rl_execute_batch(rl_engine* e, size_t n, const uint64_t* key,
                           op ? e->s_op : nullptr, e->s_allowed, e->s_remaining,
                           tokens_after ? e->s_tokens : nullptr);
     if (rc != RL_OK) { (void)hipStreamSynchronize(s); return rc; }
+    rc = collect_status(e);
+    if (rc == RL_E_INVALID_ARG && e->h_ctl->span_overflow && !e->force_wide) {
+        // the batch spans more than the compact record's 2^32 ms: it was rejected before any
+        // state was touched, so run it again in 32-B records (full now_ms)
+        e->force_wide = true;
+        rc = run_batch_device(e, n, e->s_key, e->s_permits, e->s_now, limiter ? e->s_lim : nullptr,
+                              op ? e->s_op : nullptr, e->s_allowed, e->s_remaining,
+                              tokens_after ? e->s_tokens : nullptr);
+        e->force_wide = false;
+        if (rc != RL_OK) { (void)hipStreamSynchronize(s); return rc; }
+        rc = collect_status(e);
+    }
     HIP_OK(hipMemcpyAsync(allowed, e->s_allowed, n, hipMemcpyDeviceToHost, s));
     HIP_OK(hipMemcpyAsync(remaining, e->s_remaining, n * 8, hipMemcpyDeviceToHost, s));
     if (tokens_after) HIP_OK(hipMemcpyAsync(tokens_after, e->s_tokens, n * 8, hipMemcpyDeviceToHost, s));
-    return collect_status(e);
+    HIP_OK(hipStreamSynchronize(s));
+    return rc;
 }
 
 extern "C" int rl_try_acquire_batch(rl_engine* e, size_t n, const uint64_t* key_hash,
@@ -733,6 +749,7 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "scatter_per_cu") == 0) { e->sc_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "unpermute_per_cu") == 0) { e->un_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "debug_regions") == 0) { e->debug_regions = value != 0; return RL_OK; }
+    if (std::strcmp(key, "wide_records") == 0) { e->force_wide = value != 0; return RL_OK; }
     if (std::strcmp(key, "stage_timing") == 0) {     // hipEvents around every stage on/off
         if (value) ensure_events(e);
         e->timing = value != 0;
@@ -780,12 +797,54 @@ extern "C" int rl_route_partition(rl_engine* e, size_t n, const uint64_t* key_ha
         return RL_OK;
     }
     HIP_OK(launch_owner_partition(key_hash, (uint32_t)n, shard_count, perm, e->route_counts,
-                                  e->route_scratch, s));
+                                  e->route_scratch, e->d_dir, s));
     uint32_t c[64];
     HIP_OK(hipMemcpyAsync(c, e->route_counts, shard_count * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     for (uint32_t i = 0; i < shard_count; ++i) counts_host[i] = c[i];
     return RL_OK;
+}
+
+// Hot-key owner directory: key_hash[i] is owned by owner[i] instead of its hash owner.
+// Every rank of a router must install the same directory, before any state exists for
+// those keys (or after moving it with rl_export_state / rl_import_state).
+extern "C" int rl_set_owner_directory(rl_engine* e, size_t n, const uint64_t* key_hash,
+                                      const uint32_t* owner) {
+    if (!e || (n && (!key_hash || !owner)) || n > kDirMax) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    for (size_t i = 0; i < n; ++i)
+        if (owner[i] >= e->opts.shard_count) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    if (n == 0) {
+        dfree(e->d_dir);
+        e->h_dir.clear();
+        return RL_OK;
+    }
+    std::vector<DirSlot> t(kDirSlots, DirSlot{0, kDirEmpty, 0});
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t tag = mix64(key_hash[i]);
+        uint32_t p = (uint32_t)tag & (kDirSlots - 1);
+        while (t[p].owner != kDirEmpty && t[p].tag != tag) p = (p + 1) & (kDirSlots - 1);
+        t[p].tag = tag;
+        t[p].owner = owner[i];
+    }
+    if (!e->d_dir && dalloc(&e->d_dir, kDirSlots) != RL_OK) return RL_E_NOMEM;
+    HIP_OK(hipMemcpy(e->d_dir, t.data(), kDirSlots * sizeof(DirSlot), hipMemcpyHostToDevice));
+    e->h_dir.swap(t);
+    return RL_OK;
+}
+
+extern "C" uint32_t rl_owner_of_engine(rl_engine* e, uint64_t key_hash) {
+    if (!e) return 0;
+    const uint64_t tag = mix64(key_hash);
+    if (!e->h_dir.empty()) {
+        uint32_t p = (uint32_t)tag & (kDirSlots - 1);
+        for (uint32_t i = 0; i < kDirSlots && e->h_dir[p].owner != kDirEmpty; ++i) {
+            if (e->h_dir[p].tag == tag) return e->h_dir[p].owner;
+            p = (p + 1) & (kDirSlots - 1);
+        }
+    }
+    return e->opts.shard_count <= 1 ? 0u : (uint32_t)(tag >> (64 - e->shard_bits));
 }
 
 extern "C" int rl_route_pack(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key,
@@ -947,7 +1006,7 @@ extern "C" int rl_route_partition_device(rl_engine* e, size_t n, const uint64_t*
         HIP_OK(hipMemsetAsync(e->route_counts, 0, 64 * sizeof(uint32_t), s));
     } else {
         HIP_OK(launch_owner_partition(key_hash, (uint32_t)n, shard_count, perm, e->route_counts,
-                                      e->route_scratch, s));
+                                      e->route_scratch, e->d_dir, s));
     }
     HIP_OK(launch_counts_to_header(e->route_counts, shard_count, counts_dev, (uint32_t)counts_stride, s));
     return RL_OK;

@@ -1890,9 +1890,26 @@ __global__ __launch_bounds__(256) void k_synth(SynthArgs a) {
 // Stable partition of a batch by owner shard (multi-GPU routing). One block per
 // 16K tile computes per-tile counts (upsweep), the host-side scan is done by
 // k_scan_rows, and the same tile re-ranks stably (shard_count <= 64).
+//
+// owner(h) = top log2(G) bits of mix64(h), except for the keys of the hot-key directory
+// (rl_set_owner_directory): an open-addressing table of kDirSlots {tag, owner} that places
+// the hottest keys explicitly so that one owner does not carry the top Zipf keys together.
+__device__ inline uint32_t owner_of_tag(uint64_t t, int sbits, const DirSlot* dir) {
+    if (dir) {
+        uint32_t p = (uint32_t)t & (kDirSlots - 1);
+        for (uint32_t i = 0; i < kDirSlots; ++i) {
+            const DirSlot d = dir[p];
+            if (d.owner == kDirEmpty) break;
+            if (d.tag == t) return d.owner;
+            p = (p + 1) & (kDirSlots - 1);
+        }
+    }
+    return sbits ? (uint32_t)(t >> (64 - sbits)) : 0u;
+}
+
 __global__ __launch_bounds__(kTileThreads) void k_owner_count(const uint64_t* key, uint32_t n,
                                                               int sbits, uint32_t n_tiles,
-                                                              uint32_t* counts) {
+                                                              uint32_t* counts, const DirSlot* dir) {
     __shared__ uint32_t hist[64];
     const uint32_t t = threadIdx.x;
     if (t < 64) hist[t] = 0;
@@ -1900,10 +1917,7 @@ __global__ __launch_bounds__(kTileThreads) void k_owner_count(const uint64_t* ke
     const uint32_t tile = blockIdx.x;
     for (int r = 0; r < kTileItems; ++r) {
         const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
-        if (i < n) {
-            const uint32_t o = sbits ? (uint32_t)(mix64(key[i]) >> (64 - sbits)) : 0u;
-            atomicAdd(&hist[o], 1u);
-        }
+        if (i < n) atomicAdd(&hist[owner_of_tag(mix64(key[i]), sbits, dir)], 1u);
     }
     __syncthreads();
     if (t < (1u << sbits)) counts[(size_t)t * n_tiles + tile] = hist[t];
@@ -1913,7 +1927,7 @@ __global__ __launch_bounds__(kTileThreads) void k_owner_scatter(const uint64_t* 
                                                                 int sbits, uint32_t n_tiles,
                                                                 const uint32_t* counts,
                                                                 const uint32_t* bin_base,
-                                                                uint32_t* perm) {
+                                                                uint32_t* perm, const DirSlot* dir) {
     __shared__ uint32_t cur[64];
     __shared__ uint8_t cntw[kTileThreads / 64][64];
     const uint32_t t = threadIdx.x, wid = t >> 6;
@@ -1927,7 +1941,7 @@ __global__ __launch_bounds__(kTileThreads) void k_owner_scatter(const uint64_t* 
     for (int r = 0; r < kTileItems; ++r) {
         const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
         const bool active = i < n;
-        const uint32_t d = (active && sbits) ? (uint32_t)(mix64(key[i]) >> (64 - sbits)) : 0u;
+        const uint32_t d = active ? owner_of_tag(mix64(key[i]), sbits, dir) : 0u;
         const uint64_t m = wave_match(d, sbits, active);
         const uint32_t lr = popc_below(m);
         const uint32_t c = (uint32_t)__popcll(m);
@@ -2184,6 +2198,22 @@ hipError_t launch_route_unpack_ret(uint32_t n, const uint32_t* perm, const void*
 __global__ void k_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride) {
     const uint32_t t = threadIdx.x;
     if (t < g) hdr[(size_t)t * stride] = counts[t];
+}
+
+// Router header rows {count (already there), base_ms, overflow, published status}.
+__global__ void k_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, uint32_t g) {
+    const uint32_t t = threadIdx.x;
+    if (t < g) {
+        hdr[(size_t)t * 4 + 1] = base_ovf[0];
+        hdr[(size_t)t * 4 + 2] = base_ovf[1];
+        hdr[(size_t)t * 4 + 3] = status;
+    }
+}
+
+hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, uint32_t g,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_fill_header, dim3(1), dim3(64), 0, s, hdr, base_ovf, status, g);
+    return hipGetLastError();
 }
 
 hipError_t launch_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride,
@@ -2520,17 +2550,17 @@ hipError_t launch_synth(const SynthArgs& a, hipStream_t s) {
 
 hipError_t launch_owner_partition(const uint64_t* key, uint32_t n, uint32_t shard_count,
                                   uint32_t* perm, uint32_t* counts_dev, uint32_t* scratch,
-                                  hipStream_t s) {
+                                  const DirSlot* dir, hipStream_t s) {
     int sbits = 0;
     while ((1u << sbits) < shard_count) ++sbits;
     const uint32_t nt = tiles_for(n);
     uint32_t* counts = scratch;                       // [shards][tiles]
     uint32_t* base = scratch + (size_t)shard_count * nt;
-    hipLaunchKernelGGL(k_owner_count, dim3(nt), dim3(kTileThreads), 0, s, key, n, sbits, nt, counts);
+    hipLaunchKernelGGL(k_owner_count, dim3(nt), dim3(kTileThreads), 0, s, key, n, sbits, nt, counts, dir);
     hipLaunchKernelGGL(k_scan_rows, dim3(shard_count), dim3(256), 0, s, counts, counts, nt, counts_dev);
     hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, counts_dev, base, shard_count);
     hipLaunchKernelGGL(k_owner_scatter, dim3(nt), dim3(kTileThreads), 0, s, key, n, sbits, nt,
-                       counts, base, perm);
+                       counts, base, perm, dir);
     return hipGetLastError();
 }
 

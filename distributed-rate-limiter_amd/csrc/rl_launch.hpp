@@ -101,6 +101,11 @@ struct RegionArgs {
 };
 
 constexpr int kMaxShards = 64;              // routing: shards per router
+// Hot-key owner directory (rl_set_owner_directory): at most kDirMax keys in kDirSlots slots.
+constexpr uint32_t kDirSlots = 8192;
+constexpr uint32_t kDirMax = 4096;
+constexpr uint32_t kDirEmpty = 0xFFFFFFFFu;
+struct DirSlot { uint64_t tag; uint32_t owner; uint32_t pad; };
 constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
 constexpr uint32_t kDbgWords = 8;        // debug words per bin
@@ -227,7 +232,7 @@ hipError_t launch_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_owner_partition(const uint64_t* key, uint32_t n, uint32_t shard_count,
                                   uint32_t* perm, uint32_t* counts_dev, uint32_t* scratch,
-                                  hipStream_t s);
+                                  const DirSlot* dir, hipStream_t s);
 
 hipError_t launch_route_pack(uint32_t n, const uint32_t* perm, const uint64_t* key,
                              const int32_t* permits, const int64_t* now, const uint16_t* lim,
@@ -271,5 +276,7 @@ hipError_t launch_route_unpack_ret(uint32_t n, const uint32_t* perm, const void*
                                    hipStream_t s);
 hipError_t launch_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride,
                                    hipStream_t s);
+hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, uint32_t g,
+                              hipStream_t s);
 
 }  // namespace rl

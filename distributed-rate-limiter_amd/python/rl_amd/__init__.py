@@ -43,8 +43,11 @@ EXPORTS = [
     "rl_route_pack_wire", "rl_route_unwire", "rl_result_width", "rl_route_fold_packed",
     "rl_route_unpack_packed", "rl_export_state", "rl_import_state",
     "rl_sweep_expired", "rl_route_return_bytes", "rl_route_fold_return",
-    "rl_route_unpack_return", "rl_route_partition_device",
+    "rl_route_unpack_return", "rl_route_partition_device", "rl_set_owner_directory",
+    "rl_owner_of_engine", "rl_router_create", "rl_router_step", "rl_router_finish",
+    "rl_router_plan_directory", "rl_router_destroy",
 ]
+RCCL_EXPORTS = ["rl_rccl_unique_id", "rl_transport_rccl_create", "rl_transport_rccl_destroy"]
 STATE_SW_BUCKET, STATE_TB_BUCKET = 0, 1
 # rl_state_entry (include/rl_engine.h): one live Redis key ("rl:<key>:<W>" / "tb:<key>")
 STATE_DTYPE = np.dtype([("key_hash", "<u8"), ("limiter", "<u2"), ("kind", "u1"),
@@ -157,6 +160,9 @@ def lib():
     L.rl_route_fold_return.argtypes = [vp, sz, vp, vp, vp, ctypes.c_int, u32, vp, u32, vp]
     L.rl_route_unpack_return.argtypes = [vp, sz, vp, vp, ctypes.c_int, u32, vp, u32, vp, vp, vp, vp]
     L.rl_route_partition_device.argtypes = [vp, sz, vp, u32, vp, vp, sz, vp]
+    L.rl_set_owner_directory.argtypes = [vp, sz, vp, vp]
+    L.rl_owner_of_engine.argtypes = [vp, ctypes.c_uint64]
+    L.rl_owner_of_engine.restype = u32
     _lib = L
     return L
 
@@ -445,6 +451,17 @@ class Engine:
                                             _p(lost), _p(stream))
         if st != RL_OK:
             raise RlError(st, "rl_route_unpack_return")
+
+    def set_owner_directory(self, keys, owners):
+        k = np.ascontiguousarray(keys, np.uint64)
+        o = np.ascontiguousarray(owners, np.uint32)
+        st = self._L.rl_set_owner_directory(self._h, len(k), _p(k) if len(k) else None,
+                                            _p(o) if len(o) else None)
+        if st != RL_OK:
+            raise RlError(st, "rl_set_owner_directory")
+
+    def owner_of(self, key_hash) -> int:
+        return int(self._L.rl_owner_of_engine(self._h, int(key_hash)))
 
     def route_partition_device(self, n, keys_dev, perm_dev, shard_count, counts_dev, stride,
                                stream=None):

@@ -148,7 +148,11 @@ class DeviceOps:
 
     def decide(self, m, k, p, t, lim=None):
         s = self._stream()
-        self.eng.execute_device(m, k, p, t, lim, None, self.allowed_r, self.remaining_r, stream=s)
+        self.eng.tune("wide_records", 1)         # the merged batch may span > 2^32 ms
+        try:
+            self.eng.execute_device(m, k, p, t, lim, None, self.allowed_r, self.remaining_r, stream=s)
+        finally:
+            self.eng.tune("wide_records", 0)
         self.eng.route_fold(m, self.allowed_r, self.remaining_r, self.packed_r, stream=s)
         return self.packed_r[:m]
 
@@ -180,11 +184,18 @@ class DeviceOps:
     def return_bytes(self, counts, width):
         return self.eng.route_return_bytes(counts, width, EXC_CAP)
 
-    def decide_return(self, m, k, p, t, lim, width, src_counts):
+    def decide_return(self, m, k, p, t, lim, width, src_counts, wide=False):
         """Decide the received requests; decisions in the segmented return layout (one
         segment + exception block per source)."""
         s = self._stream()
-        self.eng.execute_device(m, k, p, t, lim, None, self.allowed_r, self.remaining_r, stream=s)
+        if wide:
+            self.eng.tune("wide_records", 1)
+        try:
+            self.eng.execute_device(m, k, p, t, lim, None, self.allowed_r, self.remaining_r,
+                                    stream=s)
+        finally:
+            if wide:
+                self.eng.tune("wide_records", 0)
         nb = self.return_bytes(src_counts, width)
         self._ret_out = self._bytes(self._ret_out, nb, self.dev)
         out = self._ret_out[:nb]
@@ -279,9 +290,14 @@ class Router:
             self._a2a(wire_r, wire, rc, counts)
             if l_s is not None:
                 self._a2a(l_r, l_s, rc, counts)
-            k_r, p_r, t_r = self.ops.unwire(m, wire_r, [int(r[1]) for r in rows], rc)
+            bases = [int(r[1]) for r in rows]
+            k_r, p_r, t_r = self.ops.unwire(m, wire_r, bases, rc)
             width = self.ops.result_width()
-            out = self.ops.decide_return(m, k_r, p_r, t_r, l_r, width, rc)
+            # sources with far-apart time bases (skewed clocks): the merged batch may span
+            # more than the engine's compact 2^32 ms, so it runs in full-width records
+            live = [b for b, c in zip(bases, rc) if c]
+            far = bool(live) and max(live) - min(live) > (1 << 30)
+            out = self.ops.decide_return(m, k_r, p_r, t_r, l_r, width, rc, wide=far)
             back = self.ops.return_buffer(counts, width)
             seg = lambda c: self.ops.return_bytes([c], width)   # noqa: E731
             self._a2a(back, out, [seg(c) for c in counts], [seg(c) for c in rc])

@@ -308,11 +308,64 @@ int  rl_route_fold_return(rl_engine* e, size_t m, const uint8_t* allowed, const 
 int  rl_route_unpack_return(rl_engine* e, size_t n, const uint32_t* perm, const void* in, int width,
                             uint32_t n_seg, const uint64_t* seg_counts, uint32_t exc_cap,
                             uint8_t* allowed, int64_t* remaining, uint32_t* lost, void* stream);
+/* Hot-key owner directory (at most 4096 keys): key_hash[i] is owned by shard owner[i]
+ * instead of its hash owner, in rl_route_partition(_device) and rl_owner_of_engine. With
+ * Zipf traffic the hash owner of the top keys carries a multiple of the mean load (the top
+ * key alone draws ~11% of all requests at s = 1.1); listing the hottest keys with owners
+ * chosen to even the loads out removes that imbalance. Every rank must
+ * install the same directory before any state exists for the listed keys. n = 0 clears. */
+int  rl_set_owner_directory(rl_engine* e, size_t n, const uint64_t* key_hash,
+                            const uint32_t* owner);
+uint32_t rl_owner_of_engine(rl_engine* e, uint64_t key_hash);
 /* rl_route_partition without a host round-trip: counts[s] (int64) land in DEVICE memory at
  * counts_dev[s * counts_stride] (the router's header column), on `stream`. */
 int  rl_route_partition_device(rl_engine* e, size_t n, const uint64_t* key_hash,
                                uint32_t shard_count, uint32_t* perm, int64_t* counts_dev,
                                size_t counts_stride, void* stream);
+
+/* ---- multi-GPU router ----------------------------------------
+ * The reference's "distribution" is many app instances sharing one Redis
+ * (README.md:266-269); here each GPU owns a hash shard of the keyspace and one router per
+ * GPU moves every request to its owner and the decision back. A router wraps an engine
+ * created with rl_opts.shard_index = rank, shard_count = world (power of two <= 64).
+ *
+ * Transport: how a router reaches its peers; all buffers are device pointers and every
+ * call is enqueued on `stream` (collective: every rank makes the same calls in the same
+ * order). all_to_all_v sends send[send_off[p] .. +send_bytes[p]) to peer p and receives
+ * peer p's bytes at recv + recv_off[p]; byte counts are host arrays of `world` entries.
+ * The RCCL transport (librl_rccl.so, rl_transport_rccl_create) is the product one; tests
+ * supply an in-process loopback. Return 0 on success. */
+typedef struct rl_transport {
+    void* ctx;
+    int (*all_to_all_v)(void* ctx, const void* send, const uint64_t* send_off,
+                        const uint64_t* send_bytes, void* recv, const uint64_t* recv_off,
+                        const uint64_t* recv_bytes, void* stream);
+} rl_transport;
+
+typedef struct rl_router rl_router;
+/* max_batch: the largest per-rank n of rl_router_step (an owner may receive up to
+ * world x max_batch; its engine must accept that: rl_opts.max_batch). */
+int  rl_router_create(rl_engine* e, uint32_t world, uint32_t rank, const rl_transport* t,
+                      size_t max_batch, rl_router** out);
+/* tryAcquire over this rank's slice of the global arrival stream (device buffers; the
+ * ranks' slices are ordered by rank). Same results as one engine on the concatenated
+ * stream. One host synchronisation per step (the header exchange: RCCL takes its
+ * per-peer counts on the host). Errors are collective: an engine error on any rank is
+ * returned by EVERY rank's step two steps later (or by rl_router_finish). */
+int  rl_router_step(rl_router* r, size_t n, const uint64_t* key_hash, const int32_t* permits,
+                    const int64_t* now_ns, const uint16_t* limiter, uint8_t* allowed,
+                    int64_t* remaining, void* stream);
+/* Collective: the worst status of every rank's last batches (all ranks get the same). */
+int  rl_router_finish(rl_router* r);
+/* Hot-key directory for the whole router (collective, before any state exists for the
+ * chosen keys): each rank passes its n candidates with their request counts (e.g. the top
+ * keys of a sample of its traffic) and the total it sampled; the router merges them, keeps
+ * the k hottest and places them on owners by longest-processing-time-first over the
+ * owners' expected loads (rl_set_owner_directory on every rank). *placed = keys listed. */
+int  rl_router_plan_directory(rl_router* r, size_t n, const uint64_t* key_hash,
+                              const uint64_t* count, uint64_t sampled, uint32_t k,
+                              uint32_t* placed, void* stream);
+void rl_router_destroy(rl_router* r);
 
 /* ---- synthetic traces (bench / tests; deterministic in (seed, index)) ------ */
 #define RL_DIST_UNIFORM 0

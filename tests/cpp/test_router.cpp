@@ -1,0 +1,270 @@
+// The multi-GPU router through the C-ABI (include/rl_engine.h rl_router_*), checked
+// bit-exactly against the CPU oracle (oracle/rl_oracle.c, test infrastructure) on the
+// global arrival stream.
+//   test_router loop : G = 2 and 4 routers (threads), each with its own engine shard, on the
+//                      box's one GPU, over an in-process loopback transport; compact and wide
+//                      layouts, token-bucket time regression (exception blocks), the hot-key
+//                      directory, and a collective error (a shard's region overflows)
+//   test_router rccl : one rank over the RCCL transport (librl_rccl.so), world 1
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/rl_engine.h"
+#include "../../include/rl_rccl.h"
+
+extern "C" {   // oracle/rl_oracle.c (test infrastructure)
+struct orc_state;
+orc_state* orc_create(void);
+void orc_destroy(orc_state*);
+int orc_add_limiter(orc_state*, int algo, int64_t max, int64_t w, double refill);
+size_t orc_run(orc_state*, size_t n, const uint64_t* key, const int32_t* permits,
+               const int64_t* now_ns, const uint16_t* limiter, const uint8_t* op,
+               uint8_t* allowed, int64_t* remaining, double* tokens_after);
+}
+
+static int failures = 0;
+#define CHECK(c)                                                                      \
+    do {                                                                              \
+        if (!(c)) {                                                                   \
+            std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            ++failures;                                                               \
+        }                                                                             \
+    } while (0)
+#define HIPC(x) CHECK((x) == hipSuccess)
+
+static uint64_t mix(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
+    x ^= x >> 27; x *= 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+
+struct Trace {
+    std::vector<uint64_t> key;
+    std::vector<int32_t> permits;
+    std::vector<int64_t> now;
+    std::vector<uint16_t> lim;
+};
+
+// skewed keys (a few very hot), two limiters by key, arrival times over span_ms
+static Trace make_trace(size_t total, uint64_t seed, int64_t span_ms, bool regress) {
+    Trace t;
+    const int64_t NS = 1000000, T0 = 1700000000000LL;
+    for (size_t i = 0; i < total; ++i) {
+        const double u = (double)(mix(seed ^ (i * 0x9E3779B97F4A7C15ULL)) >> 11) * 0x1.0p-53;
+        const uint64_t rank = (uint64_t)(20000.0 * u * u * u * u);
+        t.key.push_back(mix(rank + (seed << 32)));
+        t.permits.push_back(1 + (int32_t)(mix(seed + 7 * i) % 4));
+        int64_t ms = T0 + (int64_t)((double)i * (double)span_ms / (double)total);
+        if (regress && (rank % 2) == 0 && mix(seed + 13 * i) % 200 == 0)
+            ms -= (int64_t)(mix(seed + 17 * i) % 5000);          // TB keys: late arrivals
+        t.now.push_back(ms * NS + (int64_t)(mix(i) % NS));
+        t.lim.push_back((uint16_t)(rank % 2));
+    }
+    return t;
+}
+
+// ---- in-process loopback transport: G ranks in threads on one device ---------------
+struct Loop {
+    int G;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0, gen = 0;
+    struct Post { const void* send; const uint64_t* so; const uint64_t* sb; } post[64];
+    explicit Loop(int g) : G(g) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const int g = gen;
+        if (++arrived == G) { arrived = 0; ++gen; cv.notify_all(); }
+        else cv.wait(lk, [&] { return gen != g; });
+    }
+};
+struct LoopRank { Loop* loop; int rank; };
+
+static int loop_a2av(void* ctx, const void* send, const uint64_t* so, const uint64_t* sb, void* recv,
+                     const uint64_t* ro, const uint64_t* rb, void* stream) {
+    LoopRank* lr = (LoopRank*)ctx;
+    Loop* L = lr->loop;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;      // my send bytes are ready
+    L->post[lr->rank] = {send, so, sb};
+    L->barrier();
+    int rc = 0;
+    for (int p = 0; p < L->G; ++p) {
+        const Loop::Post& q = L->post[p];
+        if (q.sb[lr->rank] != rb[p]) rc = -1;                   // protocol mismatch
+        if (rb[p] && hipMemcpyAsync((char*)recv + ro[p], (const char*)q.send + q.so[lr->rank], rb[p],
+                                    hipMemcpyDeviceToDevice, s) != hipSuccess)
+            rc = -1;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) rc = -1;
+    L->barrier();                                               // peers may reuse their buffers
+    return rc;
+}
+
+struct Result { std::vector<uint8_t> a; std::vector<int64_t> r; int finish = 0; uint32_t placed = 0; int step_rc = 0; };
+
+static const int64_t kLims[2][3] = {{1, 50, 60000}, {0, 30, 5000}};   // TB 50 @ 10/s, SW 30 / 5 s
+static const double kRefill[2] = {10.0, 0.0};
+
+static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int steps, bool dir,
+                     uint64_t capacity, Result* out, rl_transport* ext_t = nullptr) {
+    HIPC(hipSetDevice(0));
+    rl_opts o{};
+    o.device = 0; o.max_batch = (uint64_t)G * n; o.default_capacity = capacity;
+    o.shard_index = (uint32_t)rank; o.shard_count = (uint32_t)G;
+    rl_engine* e = nullptr;
+    CHECK(rl_create(&o, &e) == RL_OK);
+    for (int l = 0; l < 2; ++l) {
+        rl_limiter_config c{};
+        c.algo = (int)kLims[l][0]; c.max_permits = kLims[l][1]; c.window_ms = kLims[l][2];
+        c.refill_per_s = kRefill[l]; c.capacity = capacity;
+        uint16_t id;
+        CHECK(rl_add_limiter_ex(e, &c, &id) == RL_OK && id == l);
+    }
+    LoopRank lr{loop, rank};
+    rl_transport t{&lr, loop_a2av};
+    if (ext_t) t = *ext_t;
+    rl_router* r = nullptr;
+    CHECK(rl_router_create(e, (uint32_t)G, (uint32_t)rank, &t, n, &r) == RL_OK);
+    hipStream_t s;
+    HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    uint64_t* dk; int32_t* dp; int64_t* dt; uint16_t* dl; uint8_t* da; int64_t* dr;
+    HIPC(hipMalloc((void**)&dk, n * 8)); HIPC(hipMalloc((void**)&dp, n * 4)); HIPC(hipMalloc((void**)&dt, n * 8));
+    HIPC(hipMalloc((void**)&dl, n * 2)); HIPC(hipMalloc((void**)&da, n)); HIPC(hipMalloc((void**)&dr, n * 8));
+    if (dir) {                       // the hottest keys of this rank's whole slice as candidates
+        std::map<uint64_t, uint64_t> cnt;
+        for (int st = 0; st < steps; ++st)
+            for (size_t i = 0; i < n; ++i) cnt[tr->key[((size_t)st * G + rank) * n + i]]++;
+        std::vector<std::pair<uint64_t, uint64_t>> v(cnt.begin(), cnt.end());
+        std::sort(v.begin(), v.end(), [](auto& a, auto& b) { return a.second > b.second || (a.second == b.second && a.first < b.first); });
+        v.resize(std::min<size_t>(v.size(), 64));
+        std::vector<uint64_t> k, c;
+        for (auto& x : v) { k.push_back(x.first); c.push_back(x.second); }
+        CHECK(rl_router_plan_directory(r, k.size(), k.data(), c.data(), (uint64_t)steps * n, 16,
+                                       &out->placed, s) == RL_OK);
+    }
+    out->a.resize((size_t)steps * n);
+    out->r.resize((size_t)steps * n);
+    for (int st = 0; st < steps; ++st) {
+        const size_t b = ((size_t)st * G + rank) * n;
+        HIPC(hipMemcpyAsync(dk, &tr->key[b], n * 8, hipMemcpyHostToDevice, s));
+        HIPC(hipMemcpyAsync(dp, &tr->permits[b], n * 4, hipMemcpyHostToDevice, s));
+        HIPC(hipMemcpyAsync(dt, &tr->now[b], n * 8, hipMemcpyHostToDevice, s));
+        HIPC(hipMemcpyAsync(dl, &tr->lim[b], n * 2, hipMemcpyHostToDevice, s));
+        const int rc = rl_router_step(r, n, dk, dp, dt, dl, da, dr, s);
+        if (rc != RL_OK && out->step_rc == RL_OK) out->step_rc = rc;
+        HIPC(hipMemcpyAsync(&out->a[(size_t)st * n], da, n, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(&out->r[(size_t)st * n], dr, n * 8, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    out->finish = rl_router_finish(r);
+    rl_router_destroy(r);
+    HIPC(hipFree(dk)); HIPC(hipFree(dp)); HIPC(hipFree(dt)); HIPC(hipFree(dl)); HIPC(hipFree(da)); HIPC(hipFree(dr));
+    HIPC(hipStreamDestroy(s));
+    rl_destroy(e);
+}
+
+static void compare(const Trace& tr, int G, size_t n, int steps, const std::vector<Result>& res,
+                    const char* what) {
+    const size_t N = tr.key.size();
+    orc_state* o = orc_create();
+    for (int l = 0; l < 2; ++l) orc_add_limiter(o, (int)kLims[l][0], kLims[l][1], kLims[l][2], kRefill[l]);
+    std::vector<uint8_t> wa(N);
+    std::vector<int64_t> wr(N);
+    orc_run(o, N, tr.key.data(), tr.permits.data(), tr.now.data(), tr.lim.data(), nullptr, wa.data(),
+            wr.data(), nullptr);
+    orc_destroy(o);
+    size_t bad = 0, neg = 0;
+    for (int rank = 0; rank < G; ++rank)
+        for (int st = 0; st < steps; ++st)
+            for (size_t i = 0; i < n; ++i) {
+                const size_t g = ((size_t)st * G + rank) * n + i, l = (size_t)st * n + i;
+                if (res[rank].a[l] != wa[g] || res[rank].r[l] != wr[g]) {
+                    if (bad < 3)
+                        std::fprintf(stderr, "%s: rank %d step %d i %zu: got (%d,%lld) want (%d,%lld)\n", what,
+                                     rank, st, i, res[rank].a[l], (long long)res[rank].r[l], wa[g], (long long)wr[g]);
+                    ++bad;
+                }
+                neg += wr[g] < -3;
+            }
+    CHECK(bad == 0);
+    std::printf("%s: %zu requests, %zu mismatches, %zu out-of-range remainders\n", what, N, bad, neg);
+}
+
+static void loop_case(int G, size_t n, int steps, int64_t span_ms, bool regress, bool dir,
+                      const char* what) {
+    Trace tr = make_trace((size_t)G * n * steps, 0xC0FFEE + G + (regress ? 7 : 0), span_ms, regress);
+    Loop loop(G);
+    std::vector<Result> res(G);
+    std::vector<std::thread> th;
+    for (int rank = 0; rank < G; ++rank)
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, dir, (uint64_t)1 << 16, &res[rank], nullptr);
+    for (auto& x : th) x.join();
+    for (int rank = 0; rank < G; ++rank) {
+        CHECK(res[rank].step_rc == RL_OK);
+        CHECK(res[rank].finish == RL_OK);
+        if (dir) CHECK(res[rank].placed == 16 && res[rank].placed == res[0].placed);
+    }
+    compare(tr, G, n, steps, res, what);
+}
+
+static void loop_error_case() {
+    // a shard's table is far too small: its engine reports RL_E_CAPACITY, and every rank's
+    // router reports it (two steps later or at finish), never just the one rank
+    const int G = 2;
+    const size_t n = 20000;
+    const int steps = 4;
+    Trace tr = make_trace((size_t)G * n * steps, 0xBAD, 60000, false);
+    for (size_t i = 0; i < tr.key.size(); ++i) tr.key[i] = mix(i + 12345);   // all distinct keys
+    Loop loop(G);
+    std::vector<Result> res(G);
+    std::vector<std::thread> th;
+    for (int rank = 0; rank < G; ++rank)
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1, &res[rank], nullptr);
+    for (auto& x : th) x.join();
+    for (int rank = 0; rank < G; ++rank) {
+        const bool failed = res[rank].step_rc == RL_E_CAPACITY || res[rank].finish == RL_E_CAPACITY;
+        CHECK(failed);
+        CHECK(res[rank].step_rc == res[0].step_rc);
+    }
+    std::printf("collective error: step rc %d / %d, finish %d / %d\n", res[0].step_rc, res[1].step_rc,
+                res[0].finish, res[1].finish);
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "loop";
+    if (mode == "loop") {
+        loop_case(2, 100000, 3, 30000, false, false, "G=2 compact");
+        loop_case(4, 50000, 3, 30000, false, false, "G=4 compact");
+        loop_case(2, 50000, 2, (int64_t)1 << 36, false, false, "G=2 wide (span > 2^32 ms)");
+        loop_case(4, 50000, 3, 30000, true, false, "G=4 TB regression (exception blocks)");
+        loop_case(4, 50000, 3, 30000, false, true, "G=4 hot-key directory");
+        loop_error_case();
+    } else if (mode == "rccl") {
+        char id[RL_RCCL_ID_BYTES];
+        CHECK(rl_rccl_unique_id(id) == RL_OK);
+        rl_transport t{};
+        CHECK(rl_transport_rccl_create(id, 1, 0, 0, &t) == RL_OK);
+        const size_t n = 200000;
+        const int steps = 3;
+        Trace tr = make_trace(n * steps, 0x5CC1, 30000, true);
+        std::vector<Result> res(1);
+        Loop loop(1);
+        run_rank(1, 0, &loop, &tr, n, steps, false, (uint64_t)1 << 16, &res[0], &t);
+        CHECK(res[0].step_rc == RL_OK && res[0].finish == RL_OK);
+        compare(tr, 1, n, steps, res, "RCCL world 1");
+        rl_transport_rccl_destroy(&t);
+    }
+    std::printf("%s: %s (%d failures)\n", mode.c_str(), failures ? "FAIL" : "ok", failures);
+    return failures ? 1 : 0;
+}

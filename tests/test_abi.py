@@ -24,6 +24,18 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, name), name
 
 
+def test_rccl_transport_library_exports():
+    """librl_rccl.so (the router's RCCL transport, include/rl_rccl.h) builds and exports it all
+    (loading it needs RCCL's runtime, not a GPU)."""
+    path = os.path.join(rl_amd.PKG_DIR, "librl_rccl.so")
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(os.path.dirname(rl_amd.HEADER), "rl_rccl.h")).read(),
+                 flags=re.S)
+    assert set(re.findall(r"\b(rl_[a-z_0-9]+)\s*\(", src)) == set(rl_amd.RCCL_EXPORTS)
+    L = ctypes.CDLL(path)
+    for name in rl_amd.RCCL_EXPORTS:
+        assert hasattr(L, name), name
+
+
 def test_abi_version_and_strerror():
     L = rl_amd.lib()
     assert L.rl_abi_version() == 2

@@ -194,22 +194,38 @@ def test_two_pass_partition_many_regions():
     assert_same(got, want, "two-pass")
 
 
-def test_time_span_overflow_rejects_whole_batch():
+def test_time_span_overflow():
+    """A batch spanning more than the compact record's 2^32 ms: the device entry point
+    rejects it whole before any state is touched (RL_E_INVALID_ARG, every request -2);
+    the host entry point then re-runs it in 32-B records, exactly; rl_tune wide_records
+    makes the device entry point take it too."""
+    import torch
     lims = [[rl_amd.TB, 50, 60000, 10.0]]
     e = engine(lims)
     o = COracle(lims)
     k = rl_amd.mix64(np.arange(10, dtype=np.uint64))
     ok = (k, np.ones(10, np.int32), np.full(10, T0 * NS, np.int64), None, None)
-    a, r, t, st = e.execute(*ok)
+    e.execute(*ok)
     o.run(k, ok[1], ok[2])
     far = np.full(10, T0 * NS, np.int64)
-    far[5] = (T0 + (1 << 33)) * NS                   # ~99 days later: compact records overflow
-    a, r, t, st = e.execute(k, np.ones(10, np.int32), far)
-    assert st == rl_amd.RL_E_INVALID_ARG
-    assert (r == rl_amd.REM_INVALID).all()
-    # nothing was applied: the next batch still matches the oracle that never saw `far`
-    nxt = (k, np.full(10, 2, np.int32), np.full(10, (T0 + 1) * NS, np.int64))
-    assert_same(e.execute(*nxt)[:3], o.run(*nxt)[:3], "after rejected batch")
+    far[5] = (T0 + (1 << 33)) * NS                   # ~99 days later
+    dev = [torch.from_numpy(np.ascontiguousarray(x)).cuda()
+           for x in (k.view(np.int64), np.ones(10, np.int32), far)]
+    a = torch.empty(10, dtype=torch.uint8, device="cuda")
+    r = torch.empty(10, dtype=torch.int64, device="cuda")
+    e.execute_device(10, *dev, None, None, a, r)
+    assert e.last_status() == rl_amd.RL_E_INVALID_ARG
+    assert (r.cpu().numpy() == rl_amd.REM_INVALID).all()
+    got = e.execute(k, np.full(10, 2, np.int32), far)     # host entry: exact, in wide records
+    assert got[3] == rl_amd.RL_OK
+    assert_same(got[:3], o.run(k, np.full(10, 2, np.int32), far)[:3], "span retry")
+    e.tune("wide_records", 1)
+    nxt = (k, np.ones(10, np.int32), far + NS)
+    dev = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in (k.view(np.int64), nxt[1], nxt[2])]
+    e.execute_device(10, *dev, None, None, a, r)
+    assert e.last_status() == rl_amd.RL_OK
+    want = o.run(*nxt)
+    assert_same((a.cpu().numpy(), r.cpu().numpy(), None), want[:3], "wide_records")
 
 
 def test_invalid_requests():

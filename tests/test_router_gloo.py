@@ -56,7 +56,7 @@ class HostOps:
     def return_bytes(self, counts, width):
         return ret_layout(counts, width)[1]
 
-    def decide_return(self, m, k, p, t, lim, width, src_counts):
+    def decide_return(self, m, k, p, t, lim, width, src_counts, wide=False):
         kk = k.numpy().view(np.uint64)
         lm = None if lim is None else lim.numpy().view(np.uint16)
         a, r, _, _ = self.o.run(kk, p.numpy(), t.numpy(), lm, None, want_tokens=False)
