@@ -87,6 +87,32 @@ struct Slot {
     uint64_t a, b, c;
 };
 
+// HBM slot invariant (open addressing, linear probing from a key's 4-aligned home):
+// a slot is FREE iff its four words (and its local-cache word) are all zero; a key is
+// always found before the first free slot of its probe sequence. A slot whose state is
+// dead (no bucket live) but whose words are not all zero is a TOMBSTONE: it keeps the
+// probe chain intact and may be reused by an insert. Whole-region writers (a region
+// loaded as an LDS image, the TTL sweep, state import) rebuild the chain and write dead
+// slots as zeros; sparse region waves (few records) touch single buckets and never
+// create a hole. The only key whose dead state could be all-zero (tag 0 = mix64(0) with
+// a deleted token bucket) is written with c = kDeadMark instead, which no live state has
+// (TB: c bit 0 clear = absent bucket; SW: both counts zero).
+constexpr uint64_t kDeadMark = 2;
+__host__ __device__ inline bool slot_free(const Slot& v, uint64_t x = 0) {
+    return (v.tag | v.a | v.b | v.c | x) == 0;
+}
+// A used slot as written to HBM: never all-zero (see kDeadMark).
+__host__ __device__ inline Slot slot_used(Slot v, uint64_t x = 0) {
+    if (slot_free(v, x)) v.c = kDeadMark;
+    return v;
+}
+
+// LDS occupancy word of a region slot (k_regions)
+constexpr uint32_t kOccUsed = 1u;       // holds a key (live, or a tombstone with kOccTomb)
+constexpr uint32_t kOccTouched = 2u;    // read or written by this batch
+constexpr uint32_t kOccUnloaded = 4u;   // sparse region: bucket not fetched from HBM yet
+constexpr uint32_t kOccTomb = 8u;       // sparse region: dead slot (claimable by an insert)
+
 // ---------------------------------------------------------------- hashing
 // splitmix64 finaliser: a bijection on u64, so tags identify keys exactly.
 __host__ __device__ inline uint64_t mix64(uint64_t x) {

@@ -88,6 +88,8 @@ struct rl_engine {
     size_t hot_mark_cap = 0;
     uint32_t epoch = 0;
     uint32_t hot_threshold = 16384;         // rl_tune("hot_threshold"); 0 disables
+    uint32_t sparse_max = 96;               // rl_tune("sparse_max"): records per region up to
+                                            // which a region probes single buckets; 0 = never
     uint64_t* dbg = nullptr;                // rl_tune("debug_regions"): per-bin stamps
     size_t dbg_cap = 0;
     bool debug_regions = false;
@@ -519,6 +521,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.skew_ms = e->opts.max_skew_ms;
     ra.stats = e->d_stats;
     ra.cache = cache ? 1u : 0u;
+    ra.sparse_max = bsh == 0 ? e->sparse_max : 0u;
     if (e->debug_regions) {
         if (e->dbg_cap < (size_t)n_bins * kDbgWords) {
             dfree(e->dbg);
@@ -759,6 +762,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "hot_threshold") == 0) {      // records per region; 0 = no hot path
         if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
         e->hot_threshold = (uint32_t)value;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "sparse_max") == 0) {         // records per region; 0 = image mode only
+        if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
+        e->sparse_max = (uint32_t)value;
         return RL_OK;
     }
     if (std::strcmp(key, "bin_shift") == 0) {
@@ -1134,7 +1142,7 @@ extern "C" int rl_import_state(rl_engine* e, const rl_state_entry* in, size_t n,
         if (x->key_hash != y->key_hash) return x->key_hash < y->key_hash;
         return x->window_start_ms > y->window_start_ms;
     });
-    struct Img { uint64_t addr; uint8_t algo; Slot s; };
+    struct Img { uint64_t addr, xaddr; uint8_t algo; Slot s; };
     std::vector<Img> imgs;
     size_t taken = 0;
     for (size_t i = 0; i < n;) {
@@ -1172,6 +1180,8 @@ extern "C" int rl_import_state(rl_engine* e, const rl_state_entry* in, size_t n,
             }
             const uint32_t region = region_local(tag, e->shard_bits, L.region_bits);
             im.addr = (uint64_t)(uintptr_t)h.table + (uint64_t)region * kRegionSlots * sizeof(Slot);
+            im.xaddr = h.cache_table ? (uint64_t)(uintptr_t)h.cache_table +
+                                           (uint64_t)region * kRegionSlots * sizeof(uint64_t) : 0;
             imgs.push_back(im);
         }
         i = j;
@@ -1179,38 +1189,42 @@ extern "C" int rl_import_state(rl_engine* e, const rl_state_entry* in, size_t n,
     if (imgs.empty()) return RL_OK;
     std::stable_sort(imgs.begin(), imgs.end(), [](const Img& x, const Img& y) { return x.addr < y.addr; });
     std::vector<uint32_t> off;
-    std::vector<uint64_t> addr;
+    std::vector<uint64_t> addr, xaddr;
     std::vector<uint8_t> algo;
     std::vector<Slot> slots(imgs.size());
     for (size_t k = 0; k < imgs.size(); ++k) {
         if (k == 0 || imgs[k].addr != imgs[k - 1].addr) {
             off.push_back((uint32_t)k);
             addr.push_back(imgs[k].addr);
+            xaddr.push_back(imgs[k].xaddr);
             algo.push_back(imgs[k].algo);
         }
         slots[k] = imgs[k].s;
     }
     off.push_back((uint32_t)imgs.size());
     const size_t G = addr.size();
-    const size_t bytes = slots.size() * sizeof(Slot) + G * 8 + (G + 1) * 4 + G + 16;
+    const size_t bytes = slots.size() * sizeof(Slot) + G * 16 + (G + 1) * 4 + G + 16;
     uint8_t* d = nullptr;
     if (dalloc(&d, bytes) != RL_OK) return RL_E_NOMEM;
     Slot* d_img = (Slot*)d;
     uint64_t* d_addr = (uint64_t*)(d + slots.size() * sizeof(Slot));
-    uint32_t* d_off = (uint32_t*)(d_addr + G);
+    uint64_t* d_xaddr = d_addr + G;
+    uint32_t* d_off = (uint32_t*)(d_xaddr + G);
     uint32_t* d_fail = d_off + G + 1;
     uint8_t* d_algo = (uint8_t*)(d_fail + 1);
     int rc = RL_OK;
     uint32_t fail = 0;
     if (hipMemcpyAsync(d_img, slots.data(), slots.size() * sizeof(Slot), hipMemcpyHostToDevice, e->stream) != hipSuccess ||
         hipMemcpyAsync(d_addr, addr.data(), G * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipMemcpyAsync(d_xaddr, xaddr.data(), G * 8, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
         hipMemcpyAsync(d_off, off.data(), (G + 1) * 4, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
         hipMemcpyAsync(d_algo, algo.data(), G, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
         hipMemsetAsync(d_fail, 0, 4, e->stream) != hipSuccess)
         rc = RL_E_DEVICE;
     if (rc == RL_OK) {
         ImportArgs a{};
-        a.n_groups = (uint32_t)G; a.group_off = d_off; a.region_addr = d_addr; a.group_algo = d_algo;
+        a.n_groups = (uint32_t)G; a.group_off = d_off; a.region_addr = d_addr; a.xregion_addr = d_xaddr;
+        a.group_algo = d_algo;
         a.img = d_img; a.fail = d_fail;
         if (launch_import(a, e->stream) != hipSuccess ||
             hipMemcpyAsync(&fail, d_fail, 4, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||

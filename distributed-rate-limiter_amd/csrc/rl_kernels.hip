@@ -481,6 +481,37 @@ struct RegionLds : RegionTable {
 template <class Codec>
 struct RegionLds<Codec, false> : RegionTable {};
 
+// Sparse region (few records): the LDS table starts with every bucket kOccUnloaded and a
+// probe that reaches such a bucket faults it in from HBM (128 B, + 32 B of cache words);
+// dead slots come in as tombstones. tab == nullptr: the whole image is in LDS.
+struct SparseSrc {
+    const Slot* tab;
+    const uint64_t* xtab;             // local-cache words (nullable)
+    int64_t keep;                     // slot_live threshold (keep_from)
+    bool long_chain;                  // per lane: a probe went past two used buckets
+};
+
+template <class LdsT>
+__device__ inline void fault_bucket(const SparseSrc& sp, const DevLimiter& L, LdsT& S, uint32_t p) {
+    Slot v[4];
+    uint64_t x[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = sp.tab[p + k];
+    if constexpr (LdsT::kCache)
+        if (sp.xtab) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = sp.xtab[p + k];
+        }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool fr = slot_free(v[k], x[k]);
+        const bool lv = !fr && slot_live(L, v[k], sp.keep, x[k]);
+        S.tag[p + k] = v[k].tag; S.sa[p + k] = v[k].a; S.sb[p + k] = v[k].b; S.sc[p + k] = v[k].c;
+        if constexpr (LdsT::kCache) S.sx[p + k] = x[k];
+        S.occ[p + k] = fr ? 0u : lv ? kOccUsed : (kOccUsed | kOccTomb);
+    }
+}
+
 struct Applied {
     uint32_t j;                       // result index (padding slot for idle lanes)
     bool alw;                         // allowed
@@ -509,7 +540,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                                      uint32_t lane, const typename Codec::Rec& cur, bool valid,
                                      uint32_t j, int64_t base, uint32_t pad, uint32_t& n_allowed,
                                      uint32_t& n_invalid, uint32_t& n_caperr, uint32_t& n_rounds,
-                                     uint32_t& n_hits) {
+                                     uint32_t& n_hits, SparseSrc& sp) {
     constexpr uint32_t NS = kRegionSlots;
     constexpr bool tb = ALGO == kAlgoTB;        // per-algorithm code: nothing of the other
     constexpr bool CACHE = LdsT::kCache && !tb;
@@ -529,31 +560,58 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
     if (a.ablate & kAblNoProbe) { if (need) slot = (int32_t)home; need = false; }
     for (;;) {
         if (!__any(need)) break;
-        uint32_t cand = kNone;
+        uint32_t cand = kNone, fault = kNone;
+        bool cand_tomb = false;
         if (need) {
             // linear probing from a 4-aligned home, one 4-slot bucket per step: the key
-            // is in the chain before its first free slot (nothing is deleted mid-batch)
-            uint32_t p = home;
+            // is in the chain before its first free slot (nothing is deleted mid-batch).
+            // A sparse region may reach a bucket not loaded yet (fault it in, retry) and
+            // holds tombstones (never a hit; the first one before the free slot is reused).
+            uint32_t p = home, tomb = kNone;
             for (uint32_t step = 0; step < NS / 4; ++step) {
                 const uint4 o4 = *(const uint4*)&S.occ[p];
+                if (o4.x & kOccUnloaded) {                 // a bucket is loaded whole
+                    fault = p;
+                    sp.long_chain |= step >= 2;
+                    break;
+                }
                 const ulonglong2 t01 = *(const ulonglong2*)&S.tag[p];
                 const ulonglong2 t23 = *(const ulonglong2*)&S.tag[p + 2];
                 const uint32_t occm = (o4.x & 1u) | (o4.y & 1u) << 1 | (o4.z & 1u) << 2 |
                                       (o4.w & 1u) << 3;
-                const uint32_t hit = occm & ((t01.x == q.h ? 1u : 0u) | (t01.y == q.h ? 2u : 0u) |
-                                             (t23.x == q.h ? 4u : 0u) | (t23.y == q.h ? 8u : 0u));
+                const uint32_t tombm = (o4.x >> 3 & 1u) | (o4.y >> 3 & 1u) << 1 |
+                                       (o4.z >> 3 & 1u) << 2 | (o4.w >> 3 & 1u) << 3;
+                const uint32_t hit = occm & ~tombm &
+                                     ((t01.x == q.h ? 1u : 0u) | (t01.y == q.h ? 2u : 0u) |
+                                      (t23.x == q.h ? 4u : 0u) | (t23.y == q.h ? 8u : 0u));
                 const uint32_t freem = ~occm & 15u;
                 // first free slot vs first hit in scan order
                 const uint32_t ff = freem ? (uint32_t)__builtin_ctz(freem) : 4u;
                 const uint32_t fh = hit ? (uint32_t)__builtin_ctz(hit) : 4u;
                 if (fh < ff) { slot = (int32_t)(p + fh); need = false; break; }
-                if (ff < 4u) { cand = p + ff; break; }
+                const uint32_t tm = tombm & ((1u << ff) - 1u);
+                if (tomb == kNone && tm) tomb = p + (uint32_t)__builtin_ctz(tm);
+                if (ff < 4u) {
+                    cand = tomb != kNone ? tomb : p + ff;
+                    cand_tomb = tomb != kNone;
+                    sp.long_chain |= step >= 2;
+                    break;
+                }
                 p = (p + 4) & (NS - 1);
             }
-            if (need && cand == kNone) { need = false; failed = true; }
+            if (need && cand == kNone && fault == kNone) {
+                if (tomb != kNone) { cand = tomb; cand_tomb = true; }   // wrapped: reuse a tombstone
+                else { need = false; failed = true; }
+            }
+        }
+        if (__any(fault != kNone)) {
+            // lanes faulting the same bucket write the same words; nothing else in the
+            // wave touches an unloaded bucket
+            if (fault != kNone) fault_bucket(sp, L, S, fault);
         }
         wave_fence();
-        if (need && atomicCAS(&S.occ[cand], 0u, 1u) == 0u) {
+        const uint32_t expect = cand_tomb ? (kOccUsed | kOccTomb) : 0u;
+        if (need && cand != kNone && atomicCAS(&S.occ[cand], expect, kOccUsed) == expect) {
             S.tag[cand] = q.h; S.sa[cand] = 0; S.sb[cand] = 0; S.sc[cand] = 0;
             if constexpr (LdsT::kCache) S.sx[cand] = 0;
             slot = (int32_t)cand;
@@ -717,26 +775,45 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     uint64_t* xtab = nullptr;                       // the slots' local-cache states
     if constexpr (LdsT::kCache)
         if (L.cache_table) xtab = (uint64_t*)L.cache_table + (size_t)(region - L.region_base) * NS;
-    Slot img[NS / 64];
-    uint64_t xim[NS / 64];
+    // Few records: probe and update single buckets in HBM (128 B read + 32 B written per
+    // distinct key) instead of moving the 8 KB image both ways.
+    const bool sparse = RPB == 1 && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
+    SparseSrc sp{sparse ? tab : nullptr, xtab, batch_min, false};
+    // rebuild the LDS table from registers: linear probing from each key's home
+    auto rebuild = [&](const Slot (&img)[NS / 64], const uint64_t (&xim)[NS / 64], const bool (&keep)[NS / 64]) {
 #pragma unroll
-    for (uint32_t i = 0; i < NS / 64; ++i) {
-        S.occ[lane + 64 * i] = 0;
-        img[i] = tab[lane + 64 * i];
-        xim[i] = xtab ? xtab[lane + 64 * i] : 0;
-    }
-    wave_fence();
+        for (uint32_t i = 0; i < NS / 64; ++i) S.occ[lane + 64 * i] = 0;
+        wave_fence();
 #pragma unroll
-    for (uint32_t i = 0; i < NS / 64; ++i) {
-        const Slot v = img[i];
-        if (slot_live(L, v, batch_min, xim[i])) {
-            uint32_t p = slot_home(v.tag);
-            while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
-            S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
-            if constexpr (LdsT::kCache) S.sx[p] = xim[i];
+        for (uint32_t i = 0; i < NS / 64; ++i) {
+            const Slot v = img[i];
+            if (keep[i]) {
+                uint32_t p = slot_home(v.tag);
+                while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+                S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
+                if constexpr (LdsT::kCache) S.sx[p] = xim[i];
+            }
         }
+        wave_fence();
+    };
+    if (sparse) {
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) S.occ[lane + 64 * i] = kOccUnloaded;
+        wave_fence();
+    } else {
+        // load the region, dropping entries no request of this batch can see
+        Slot img[NS / 64];
+        uint64_t xim[NS / 64];
+        bool keep[NS / 64];
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) {
+            img[i] = tab[lane + 64 * i];
+            xim[i] = xtab ? xtab[lane + 64 * i] : 0;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) keep[i] = slot_live(L, img[i], batch_min, xim[i]);
+        rebuild(img, xim, keep);
     }
-    wave_fence();
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_hits = 0;
     const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -750,7 +827,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
             if constexpr (RPB == 1) {
                 // the bin is the region: every record is ours, applied straight from registers
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, idx < end, idx, base, pad,
-                                                     n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
+                                                     n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             } else {
@@ -769,7 +846,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 if (count >= 64) {
                     const uint32_t ri = (head + lane) % kRing;
                     ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
-                                           n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
+                                           n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
                     head = (head + 64) % kRing;
                     count -= 64;
                 }
@@ -797,7 +874,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 const bool v = lane < count;
                 const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
                 const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
-                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
+                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
@@ -806,17 +883,45 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     if (L.algo == kAlgoTB) stream(std::integral_constant<int, kAlgoTB>{});
     else stream(std::integral_constant<int, kAlgoSW>{});
     wave_fence();
-    // ---- write the region back (free slots as zeros)
     uint32_t touched = 0;
+    for (uint32_t s = lane; s < NS; s += 64) touched += (S.occ[s] & kOccTouched) ? 1u : 0u;
+    bool whole = !sparse;
+    if (sparse && __any(sp.long_chain)) {
+        // probe chains have grown long (tombstones accumulate while a region only ever sees
+        // few records): fault in the rest of the region (one bucket per lane), keep its live
+        // keys and rebuild it as an image region does, then write it back whole
+        if (S.occ[4 * lane] & kOccUnloaded) fault_bucket(sp, L, S, 4 * lane);
+        wave_fence();
+        Slot img[NS / 64];
+        uint64_t xim[NS / 64];
+        bool keep[NS / 64];
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) {
+            const uint32_t s = lane + 64 * i;
+            const uint32_t o = S.occ[s];
+            keep[i] = (o & kOccUsed) && !(o & kOccTomb);
+            img[i] = Slot{S.tag[s], S.sa[s], S.sb[s], S.sc[s]};
+            xim[i] = 0;
+            if constexpr (LdsT::kCache) xim[i] = S.sx[s];
+        }
+        wave_fence();
+        rebuild(img, xim, keep);
+        whole = true;
+    }
+    // ---- write the region back: every slot (free ones as zeros), or in a sparse region
+    // only the slots this batch touched
     for (uint32_t s = lane; s < NS; s += 64) {
         const uint32_t o = S.occ[s];
-        Slot v;
-        if (o & 1u) { v.tag = S.tag[s]; v.a = S.sa[s]; v.b = S.sb[s]; v.c = S.sc[s]; }
-        else { v.tag = 0; v.a = 0; v.b = 0; v.c = 0; }
+        if (!whole && !(o & kOccTouched)) continue;
+        Slot v{0, 0, 0, 0};
+        uint64_t x = 0;
+        if (o & kOccUsed) {
+            if constexpr (LdsT::kCache) x = S.sx[s];
+            v = slot_used(Slot{S.tag[s], S.sa[s], S.sb[s], S.sc[s]}, x);
+        }
         tab[s] = v;
         if constexpr (LdsT::kCache)
-            if (xtab) xtab[s] = (o & 1u) ? S.sx[s] : 0;
-        touched += (o >> 1) & 1u;
+            if (xtab) xtab[s] = x;
     }
     for (int off = 32; off > 0; off >>= 1) {
         n_allowed += __shfl_xor(n_allowed, off, 64);
@@ -1434,12 +1539,13 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         constexpr int A = decltype(algo)::value;
         const uint64_t c_p2 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
         uint32_t head = 0, count = 0;                     // LDS ring (wave-uniform)
+        SparseSrc sp{nullptr, nullptr, 0, false};         // the whole image is in LDS
         auto apply64 = [&](uint32_t valid_n) {
             const bool v = lane < valid_n;
             const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
             uint32_t n_hits = 0;                          // (no local cache on the hot path)
             const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
-                                                    pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits);
+                                                    pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
             if (v) {
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
@@ -1519,9 +1625,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     uint32_t touched = 0;
     for (uint32_t sl = lane; sl < NS; sl += 64) {
         const uint32_t o = S.occ[sl];
-        Slot v;
-        if (o & 1u) { v.tag = S.tag[sl]; v.a = S.sa[sl]; v.b = S.sb[sl]; v.c = S.sc[sl]; }
-        else { v.tag = 0; v.a = 0; v.b = 0; v.c = 0; }
+        Slot v{0, 0, 0, 0};
+        if (o & kOccUsed) v = slot_used(Slot{S.tag[sl], S.sa[sl], S.sb[sl], S.sc[sl]});
         tab[sl] = v;
         touched += (o >> 1) & 1u;
     }
@@ -2268,65 +2373,119 @@ __global__ __launch_bounds__(256) void k_export(const Slot* __restrict__ tab, ui
         if (k + (uint32_t)j < cap) out[k + j] = r[j];
 }
 
-// Import: one wave per region that receives entries. The wave stages the region's 256
-// slots in LDS, applies its keys in order (replace the slot holding the key's tag, else
-// claim the first slot whose state is absent), and writes the region back. Regions are
-// rebuilt from their live slots whenever a batch loads them, so any free slot will do.
+// Whole-region rewrite shared by the state import and the TTL sweep: one wave stages the
+// region's 256 slots, keeps those `keep` accepts, rebuilds the probe chains in LDS
+// (linear probing from each key's home, as a batch's region load does) and later writes
+// every slot back, so the HBM slot invariant (rl_device.hpp, slot_free) holds afterwards.
+struct RegionStage {
+    alignas(16) uint64_t tag[kRegionSlots];
+    uint64_t sa[kRegionSlots], sb[kRegionSlots], sc[kRegionSlots], sx[kRegionSlots];
+    uint32_t occ[kRegionSlots];
+};
+
+template <class Keep>
+__device__ inline uint32_t stage_region(RegionStage& S, const Slot* tab, const uint64_t* xt,
+                                        uint32_t lane, Keep keep) {
+    constexpr uint32_t NS = kRegionSlots;
+    Slot img[NS / 64];
+    uint64_t xim[NS / 64];
+    bool kp[NS / 64];
+    uint32_t dropped = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < NS / 64; ++i) {
+        img[i] = tab[lane + 64 * i];
+        xim[i] = xt ? xt[lane + 64 * i] : 0;
+        kp[i] = !slot_free(img[i], xim[i]) && keep(img[i], xim[i]);
+        dropped += (!slot_free(img[i], xim[i]) && !kp[i]) ? 1u : 0u;
+        S.occ[lane + 64 * i] = 0;
+    }
+    wave_fence();
+#pragma unroll
+    for (uint32_t i = 0; i < NS / 64; ++i) {
+        if (!kp[i]) continue;
+        uint32_t p = slot_home(img[i].tag);
+        while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+        S.tag[p] = img[i].tag; S.sa[p] = img[i].a; S.sb[p] = img[i].b; S.sc[p] = img[i].c;
+        S.sx[p] = xim[i];
+    }
+    wave_fence();
+    return dropped;
+}
+
+__device__ inline void write_region(const RegionStage& S, Slot* tab, uint64_t* xt, uint32_t lane) {
+    for (uint32_t k = lane; k < kRegionSlots; k += 64) {
+        Slot v{0, 0, 0, 0};
+        uint64_t x = 0;
+        if (S.occ[k] & kOccUsed) {
+            x = S.sx[k];
+            v = slot_used(Slot{S.tag[k], S.sa[k], S.sb[k], S.sc[k]}, x);
+        }
+        tab[k] = v;
+        if (xt) xt[k] = x;
+    }
+}
+
+// Import: one wave per region that receives entries. The region's present slots are
+// staged and rebuilt, then its keys are applied in order: replace the slot holding the
+// key's tag, else claim the first free slot of the key's probe sequence.
 __global__ __launch_bounds__(64) void k_import(ImportArgs a) {
-    __shared__ Slot S[kRegionSlots];
+    __shared__ RegionStage S;
+    constexpr uint32_t NS = kRegionSlots;
     const uint32_t g = blockIdx.x, lane = threadIdx.x;
     if (g >= a.n_groups) return;
     Slot* tab = (Slot*)(uintptr_t)a.region_addr[g];
-    const bool tb = a.group_algo[g] == kAlgoTB;
-    for (uint32_t k = lane; k < kRegionSlots; k += 64) S[k] = tab[k];
-    wave_fence();
+    const int algo = a.group_algo[g];
+    uint64_t* xt = (uint64_t*)(uintptr_t)a.xregion_addr[g];
+    stage_region(S, tab, xt, lane,
+                 [&](const Slot& v, uint64_t x) { return x != 0 || state_present(algo, v.b, v.c); });
     for (uint32_t j = a.group_off[g]; j < a.group_off[g + 1]; ++j) {
         const Slot im = a.img[j];
-        uint64_t hit = 0, fre = 0;
-        int32_t first_hit = -1, first_free = -1;
-        for (uint32_t b = 0; b < kRegionSlots / 64; ++b) {
-            const Slot& v = S[b * 64 + lane];
-            const bool absent = tb ? !(v.c & 1u) : v.b == 0;
-            hit = __ballot(v.tag == im.tag);
-            fre = __ballot(absent);
-            if (first_hit < 0 && hit) first_hit = (int32_t)(b * 64 + __builtin_ctzll(hit));
-            if (first_free < 0 && fre) first_free = (int32_t)(b * 64 + __builtin_ctzll(fre));
+        const uint32_t home = slot_home(im.tag);
+        int32_t p = -1;
+        for (uint32_t b = 0; b < NS / 64 && p < 0; ++b) {    // probe order = (b, lane)
+            const uint32_t s = (home + b * 64 + lane) & (NS - 1);
+            const bool used = (S.occ[s] & kOccUsed) != 0;
+            const uint64_t fre = __ballot(!used);
+            const uint64_t hit = __ballot(used && S.tag[s] == im.tag);
+            const uint64_t before = fre ? ((fre & (0 - fre)) - 1) | (fre & (0 - fre)) : ~0ULL;
+            const uint64_t h = hit & before;                  // a hit before the first free slot
+            if (h) p = (int32_t)((home + b * 64 + (uint32_t)__builtin_ctzll(h)) & (NS - 1));
+            else if (fre) p = (int32_t)((home + b * 64 + (uint32_t)__builtin_ctzll(fre)) & (NS - 1));
         }
-        const int32_t p = first_hit >= 0 ? first_hit : first_free;
         if (p < 0) {
             if (lane == 0) atomicAdd(a.fail, 1u);
         } else if (lane == 0) {
-            S[p] = im;
+            S.occ[p] = kOccUsed;
+            S.tag[p] = im.tag; S.sa[p] = im.a; S.sb[p] = im.b; S.sc[p] = im.c; S.sx[p] = 0;
         }
         wave_fence();
     }
-    for (uint32_t k = lane; k < kRegionSlots; k += 64) tab[k] = S[k];
+    write_region(S, tab, xt, lane);
 }
 
-// TTL sweep: one thread per slot; a slot none of whose buckets is live at `now` is zeroed
-// (the criterion the region load applies, slot_live). One counter atomic per wave.
-__global__ __launch_bounds__(256) void k_sweep(Slot* __restrict__ tab, uint64_t n_slots,
-                                               DevLimiter L, int64_t now, uint32_t* count) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool dead = false;
-    if (i < n_slots) {
-        const Slot v = tab[i];
-        uint64_t* xt = (uint64_t*)L.cache_table;
-        const uint64_t x = xt ? xt[i] : 0;
-        dead = (v.tag | v.a | v.b | v.c) != 0 && !slot_live(L, v, now, x);
-        if (dead) {
-            tab[i] = Slot{0, 0, 0, 0};
-            if (xt) xt[i] = 0;
-        }
-    }
-    const uint64_t m = __ballot(dead);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (uint32_t)__popcll(m));
+// TTL sweep: one wave per region; every used slot none of whose buckets is live at `now`
+// (slot_live, the criterion a batch's region load applies) is dropped and the region is
+// rebuilt (no tombstone survives a sweep). One counter atomic per wave.
+__global__ __launch_bounds__(64) void k_sweep(Slot* __restrict__ tab0, uint64_t n_regions,
+                                              DevLimiter L, int64_t now, uint32_t* count) {
+    __shared__ RegionStage S;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t r = blockIdx.x;
+    if (r >= n_regions) return;
+    Slot* tab = tab0 + r * kRegionSlots;
+    uint64_t* xt = L.cache_table ? (uint64_t*)L.cache_table + r * kRegionSlots : nullptr;
+    uint32_t dead = stage_region(S, tab, xt, lane,
+                                 [&](const Slot& v, uint64_t x) { return slot_live(L, v, now, x); });
+    write_region(S, tab, xt, lane);
+    for (int o = 32; o > 0; o >>= 1) dead += __shfl_xor(dead, o, 64);
+    if (lane == 0 && dead) atomicAdd(count, dead);
 }
 
 hipError_t launch_sweep(Slot* table, uint64_t n_slots, const DevLimiter& L, int64_t now_ms,
                         uint32_t* count, hipStream_t s) {
-    const uint64_t blocks = (n_slots + 255) / 256;
-    hipLaunchKernelGGL(k_sweep, dim3((uint32_t)blocks), dim3(256), 0, s, table, n_slots, L, now_ms,
+    const uint64_t regions = n_slots / kRegionSlots;
+    if (regions == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sweep, dim3((uint32_t)regions), dim3(64), 0, s, table, regions, L, now_ms,
                        count);
     return hipGetLastError();
 }

@@ -84,6 +84,8 @@ struct RegionArgs {
     int64_t skew_ms;           // rl_opts.max_skew_ms: slots kept until dead at batch min - skew
     unsigned long long* stats; // [kStatSlots][8] sharded batch counters (k_stats_reduce)
     uint32_t cache;            // some limiter keeps a local cache (k_regions<..., CACHE>)
+    uint32_t sparse_max;       // one region per bin: a region with <= this many records
+                               // probes single buckets in HBM instead of loading its image
     const uint32_t* rend;      // nullable: bin b holds records [rstart[b], rend[b]) (2 passes)
     // hot regions (bin_shift 0): k_hot_select lists the largest bins (>= hot_threshold
     // records, at most kHotMax); the k_hot_* kernels own them (hot_mark[bin] == epoch),
@@ -198,6 +200,7 @@ struct ImportArgs {
     uint32_t n_groups;
     const uint32_t* group_off;     // [n_groups + 1] into img
     const uint64_t* region_addr;   // [n_groups] device address of the region's 256 slots
+    const uint64_t* xregion_addr;  // [n_groups] its local-cache words (0: none)
     const uint8_t* group_algo;     // [n_groups]
     const Slot* img;               // slot images, grouped by region
     uint32_t* fail;                // keys that found no free slot
