@@ -73,7 +73,7 @@ struct DevLimiter {          // 96 B, read-only during a batch
     double inv_window;       // 1.0 / w: first guess of Java's now / w (jdiv corrects it)
     uint64_t cache_table;    // SW local cache: one u64 per slot (block-until ms), or 0
     int64_t cache_ttl_ms;    // localCacheTtl (0: no local cache, the parity-mode default)
-    uint64_t pad1;
+    double inv_rate;         // TB: 1 / rate_per_ms (first guesses only, never a decision)
 };
 
 // One 32-byte slot of a region (HBM and the LDS image).

@@ -304,6 +304,7 @@ extern "C" int rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* c, uint1
     d.window_ms = c->window_ms;
     d.ttl_ms = c->algo == RL_ALGO_TOKEN_BUCKET ? c->window_ms * 2 : c->window_ms;
     d.rate_per_ms = c->refill_per_s / 1000.0;        // TokenBucketRateLimiter.java:85
+    d.inv_rate = d.rate_per_ms > 0.0 ? 1.0 / d.rate_per_ms : 0.0;
     d.inv_window = 1.0 / (double)c->window_ms;
     d.capacity = (double)c->max_permits;
     h.table_bytes = (size_t)(1ULL << k) * kRegionSlots * sizeof(Slot);

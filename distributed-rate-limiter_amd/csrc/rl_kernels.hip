@@ -481,6 +481,11 @@ struct RegionLds : RegionTable {
 template <class Codec>
 struct RegionLds<Codec, false> : RegionTable {};
 
+#ifndef RL_NO_SPARSE
+#define RL_NO_SPARSE 0                    // A/B builds: 1 compiles the sparse-region path out
+#endif
+constexpr bool kSparseOn = !RL_NO_SPARSE;
+
 // Sparse region (few records): the LDS table starts with every bucket kOccUnloaded and a
 // probe that reaches such a bucket faults it in from HBM (128 B, + 32 B of cache words);
 // dead slots come in as tombstones. tab == nullptr: the whole image is in LDS.
@@ -570,7 +575,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             uint32_t p = home, tomb = kNone;
             for (uint32_t step = 0; step < NS / 4; ++step) {
                 const uint4 o4 = *(const uint4*)&S.occ[p];
-                if (o4.x & kOccUnloaded) {                 // a bucket is loaded whole
+                if (kSparseOn && (o4.x & kOccUnloaded)) {  // a bucket is loaded whole
                     fault = p;
                     sp.long_chain |= step >= 2;
                     break;
@@ -579,8 +584,8 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 const ulonglong2 t23 = *(const ulonglong2*)&S.tag[p + 2];
                 const uint32_t occm = (o4.x & 1u) | (o4.y & 1u) << 1 | (o4.z & 1u) << 2 |
                                       (o4.w & 1u) << 3;
-                const uint32_t tombm = (o4.x >> 3 & 1u) | (o4.y >> 3 & 1u) << 1 |
-                                       (o4.z >> 3 & 1u) << 2 | (o4.w >> 3 & 1u) << 3;
+                const uint32_t tombm = !kSparseOn ? 0u : (o4.x >> 3 & 1u) | (o4.y >> 3 & 1u) << 1 |
+                                                         (o4.z >> 3 & 1u) << 2 | (o4.w >> 3 & 1u) << 3;
                 const uint32_t hit = occm & ~tombm &
                                      ((t01.x == q.h ? 1u : 0u) | (t01.y == q.h ? 2u : 0u) |
                                       (t23.x == q.h ? 4u : 0u) | (t23.y == q.h ? 8u : 0u));
@@ -604,7 +609,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 else { need = false; failed = true; }
             }
         }
-        if (__any(fault != kNone)) {
+        if (kSparseOn && __any(fault != kNone)) {
             // lanes faulting the same bucket write the same words; nothing else in the
             // wave touches an unloaded bucket
             if (fault != kNone) fault_bucket(sp, L, S, fault);
@@ -777,7 +782,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         if (L.cache_table) xtab = (uint64_t*)L.cache_table + (size_t)(region - L.region_base) * NS;
     // Few records: probe and update single buckets in HBM (128 B read + 32 B written per
     // distinct key) instead of moving the 8 KB image both ways.
-    const bool sparse = RPB == 1 && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
+    const bool sparse = kSparseOn && RPB == 1 && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
     SparseSrc sp{sparse ? tab : nullptr, xtab, batch_min, false};
     // rebuild the LDS table from registers: linear probing from each key's home
     auto rebuild = [&](const Slot (&img)[NS / 64], const uint64_t (&xim)[NS / 64], const bool (&keep)[NS / 64]) {
@@ -955,27 +960,18 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
 //    at or after the newest bucket, and the TB balance (Lua :46-58) is non-decreasing.
 // So one threshold pair [T0, T1) per state holds exactly the times at which a request is
 // denied with remaining 0 (SW: est >= max; TB: 0 <= balance < 1), whatever its permits.
-// Requests outside it (the next allow, denials with remaining > 0, peeks, resets) run
-// the exact step one at a time in arrival order; after a state change T1 is found again
-// by an exact search that evaluates the very same arithmetic (tb_refill, sw_estimate) at
-// 64 times per wave instruction. Three phases:
+// Inside an undecided chunk the further thresholds T_2.. decide the other denials by
+// integer compares (hot_pred_k below); the allowed request, a peek or a reset runs the
+// exact step alone, and after each state change the thresholds are found again by an
+// exact search that evaluates the very same arithmetic (tb_refill, sw_estimate) at 64
+// times per wave instruction. Three phases:
 //  A  k_hot_summ  (all CUs)  per 64 records: time range of the hot key's plain acquires,
 //                             count of records that need the exact path;
 //  B  k_hot_chain (one wave per hot region, beside k_regions) walks the summaries with
 //                             [T0, T1), decides whole chunks unread, processes the rest
 //                             record by record (other keys through wave_apply);
 //  C  k_hot_fill  (all CUs)  writes the results of the decided chunks.
-template <int ALGO>
-__device__ inline bool hot_pred(const DevLimiter& L, int64_t t, uint64_t a, uint64_t b, uint64_t c) {
-    if constexpr (ALGO == kAlgoTB) {
-        return tb_refill(L, t, a, b, c) >= 1.0;
-    } else {
-        const SW2 s = sw_unpack(a, b, c);
-        return sw_estimate(s, sw_geo(t, L), t, L.window_ms) < L.max_permits;
-    }
-}
-
-// Start of the range on which hot_pred is monotone and the fast result is valid.
+// Start of the range on which the thresholds (hot_pred_k) are monotone and valid.
 template <int ALGO>
 __device__ inline int64_t hot_t0(int64_t lo, int64_t hi, uint64_t a, uint64_t b, uint64_t c) {
     if constexpr (ALGO == kAlgoTB) {
@@ -1018,65 +1014,76 @@ __device__ inline int64_t wave_first_true(int64_t s, int64_t hi, uint32_t lane, 
     return lo;
 }
 
-// Approximate first t >= s with hot_pred(t) from the closed forms (only a starting
-// point: hot_thresholds checks it exactly). Returns s when there is no useful estimate.
+// For a fixed state and t >= hot_t0, an acquire of k permits at t is allowed iff t >= T_k,
+// the first t with (TB) balance >= k or (SW) estimate <= max - k: the predicate below is
+// monotone in t (nested in k).
 template <int ALGO>
-__device__ inline int64_t hot_t1_guess(const DevLimiter& L, int64_t s, uint64_t a, uint64_t b,
-                                       uint64_t c) {
+__device__ inline bool hot_pred_k(const DevLimiter& L, int64_t t, uint64_t a, uint64_t b, uint64_t c,
+                                  int64_t k) {
+    if constexpr (ALGO == kAlgoTB) {
+        return tb_refill(L, t, a, b, c) >= (double)k;
+    } else {
+        const SW2 s = sw_unpack(a, b, c);
+        return sw_estimate(s, sw_geo(t, L), t, L.window_ms) + k <= L.max_permits;
+    }
+}
+
+// A starting point for T_k from the closed forms (hot_t1_lb checks it exactly).
+template <int ALGO>
+__device__ inline int64_t hot_tk_guess(const DevLimiter& L, int64_t s, uint64_t a, uint64_t b,
+                                       uint64_t c, int64_t k) {
     if constexpr (ALGO == kAlgoTB) {
         if (!(c & 1u)) return s;                                // absent: full at every t
         const double tok0 = __longlong_as_double((long long)a);
         const int64_t last = (int64_t)b;
-        if (!(tok0 < 1.0) || !(L.rate_per_ms > 0.0)) return s;
-        const double te = (double)last + ceil((1.0 - tok0) / L.rate_per_ms);
-        int64_t g = te < 4.0e18 ? (int64_t)te : INT64_MAX / 4;
+        if (!(tok0 < (double)k) || !(L.rate_per_ms > 0.0)) return s;
+        const double te = (double)last + ceil(((double)k - tok0) * L.inv_rate);
+        const int64_t g = te < 4.0e18 ? (int64_t)te : INT64_MAX / 4;
         const int64_t full = last + L.ttl_ms + 1;               // expired: full again
         return g < full ? g : full;
     } else {
+        const int64_t m = L.max_permits - k + 1;                // allowed iff estimate < m
         const int64_t w = L.window_ms;
         const SW2 st = sw_unpack(a, b, c);
         const SWGeo g0 = sw_geo(s, L);
         const int64_t C = sw_get(st, g0.curr_start, s, w);
         const int64_t P = sw_get(st, g0.prev_start, s, w);
-        if (C >= L.max_permits || P == 0) return s;
-        const double rr = (double)w * (1.0 - (double)(L.max_permits - C) / (double)P);
-        int64_t g = g0.curr_start + (int64_t)floor(rr) + 1;
-        int64_t lastp = INT64_MAX / 4;                          // previous bucket's TTL lapse
-        if (st.b1_start == g0.prev_start) lastp = st.b1_start + st.b1_off;
-        else if (st.b1_start == g0.curr_start) lastp = g0.prev_start + st.b0_off;
-        if (g > lastp + w + 1) g = lastp + w + 1;
         const int64_t wend = g0.curr_start + w;                 // next window: a new geometry
-        return g < wend ? g : wend;
+        if (m <= 0) return s;
+        if (C < m) {
+            if (P == 0) return s;
+            // estimate = P * pw + C < m  <=>  now % w > w (1 - (m - C) / P)
+            const double rr = (double)w * (1.0 - (double)(m - C) * __builtin_amdgcn_rcp((double)P));
+            int64_t g = g0.curr_start + (int64_t)floor(rr) + 1;
+            int64_t lastp = INT64_MAX / 4;                      // previous bucket's TTL lapse
+            if (st.b1_start == g0.prev_start) lastp = st.b1_start + st.b1_off;
+            else if (st.b1_start == g0.curr_start) lastp = g0.prev_start + st.b0_off;
+            if (g > lastp + w + 1) g = lastp + w + 1;
+            if (g < wend) return g > s ? g : s;
+        }
+        // not in this window: in the next one the current bucket (C) is the previous one,
+        // weighted by pw, until its TTL lapses (last INCR + w)
+        if (C < m) return wend;
+        const int64_t lastc = st.b1_start == g0.curr_start ? st.b1_start + st.b1_off : wend;
+        const double rr = (double)w * (1.0 - (double)m * __builtin_amdgcn_rcp((double)C));
+        int64_t g = wend + (int64_t)floor(rr) + 1;
+        if (g > lastc + w + 1) g = lastc + w + 1;
+        return g;
     }
 }
 
+// A lower bound T1 > T0 of the first t >= T0 at which an acquire of one permit is
+// allowed, from the closed-form guess g checked exactly at g - 1 (the predicate is monotone
+// on [T0, hi]); T0 (an empty range) when the check fails. [T0, T1) then holds only denials
+// with remaining 0; whatever lies beyond it is processed exactly.
 template <int ALGO>
-__device__ inline void hot_thresholds(const DevLimiter& L, uint64_t a, uint64_t b, uint64_t c,
-                                      int64_t from, int64_t lo, int64_t hi, uint32_t lane,
-                                      int64_t* T0, int64_t* T1) {
-    const int64_t t0 = hot_t0<ALGO>(lo, hi, a, b, c);
-    const int64_t s = from > t0 ? from : t0;
-    auto pred = [&](int64_t t) { return hot_pred<ALGO>(L, t, a, b, c); };
-    int64_t t1 = hi + 1;
-    bool found = false;
-    // First an estimate from the closed form of the refill / the window weight, checked
-    // exactly at the 64 times around it (one ballot: the predicate is monotone, so a
-    // false -> true step inside the probed times is the answer); the full search only if
-    // the step lies outside them.
-    int64_t g = hot_t1_guess<ALGO>(L, s, a, b, c);
-    if (g > s + 32) {
-        int64_t t = g - 32 + (int64_t)lane;
-        if (t > hi) t = hi;
-        const uint64_t m = __ballot(pred(t));
-        if (m != 0 && !(m & 1u)) {
-            t1 = __shfl(t, (int)__builtin_ctzll(m), 64);
-            found = true;
-        }
-    }
-    if (!found) t1 = wave_first_true(s, hi, lane, pred);
-    if (t1 == s) t1 = t0;        // pred(s) already true: [t0, s) undecided -> empty range
-    *T0 = t0;
-    *T1 = t1;
+__device__ inline int64_t hot_t1_lb(const DevLimiter& L, uint64_t a, uint64_t b, uint64_t c,
+                                    int64_t T0, int64_t hi) {
+    if (T0 > hi) return T0;
+    int64_t g = hot_tk_guess<ALGO>(L, T0, a, b, c, 1);
+    if (g > hi + 1) g = hi + 1;
+    if (g <= T0 + 1) return T0;
+    return hot_pred_k<ALGO>(L, g - 1, a, b, c, 1) ? T0 : g;
 }
 
 // Lane order = arrival order; chunk g of the listed regions -> (region i, chunk c).
@@ -1321,19 +1328,23 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     };
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0, n_other = 0;
+    uint32_t n_changed = 0, n_tk = 0, n_fb = 0;       // debug: changes, [T0, T1) updates
     uint64_t cyc_run = 0, cyc_search = 0, cyc_detail = 0, cyc_pass2 = 0;   // debug stamps
     bool any_hot = false;
     auto pass1 = [&](auto algo) {
         constexpr int A = decltype(algo)::value;
-        int64_t T0 = lo, T1 = lo;                         // empty range until computed
-        hot_thresholds<A>(L, S.sa[hs], S.sb[hs], S.sc[hs], lo, lo, hi, lane, &T0, &T1);
-        // the hot records of one chunk, one by one (lane = arrival order inside the chunk).
-        // The next chunk's records are prefetched: undecided chunks come in runs (an allow,
-        // then the request that finds the key at its limit again).
+        // the hot key's state (registers; written to LDS when it changes) and the range
+        // [T0, T1) in which every acquire is denied with remaining 0 (whole chunks and groups
+        // inside it are decided without being read)
+        uint64_t sa = S.sa[hs], sb = S.sb[hs], sc = S.sc[hs];
+        int64_t T0 = hot_t0<A>(lo, hi, sa, sb, sc);
+        int64_t T1 = hot_t1_lb<A>(L, sa, sb, sc, T0, hi);
+        // the hot records of one chunk (lane = arrival order inside the chunk). The next
+        // chunk's records are prefetched: undecided chunks come in runs.
         Rec pre = recs[min(f.start + lane, f.end - 1)];
         uint32_t pre_c = 0;
         uint32_t prev_detail = 0xFFFFFFF0u;               // last chunk processed here
-        bool stale = false;                               // [T0, T1) emptied, not searched
+        bool stale = false;                               // [T0, T1) emptied, not recomputed
         auto detail = [&](uint32_t c) {
             ++n_detail;
             const uint64_t c_det = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
@@ -1358,112 +1369,140 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
                 if (pend && lane < first) {               // inside [T0, T1): denied, remaining 0
                     orem = 0;
-                    if (TOK && A == kAlgoTB) tk = tb_refill(L, q.now_ms, S.sa[hs], S.sb[hs], S.sc[hs]);
+                    if (TOK && A == kAlgoTB) tk = tb_refill(L, q.now_ms, sa, sb, sc);
                     pend = false;
                 }
             }
-            if (__any(pend)) {
-                // The rest of the key's requests in this chunk, in rounds (as wave_apply,
-                // all lanes are one key): (D) the prefix up to the first state change, or
-                // (A, sliding window) up to the first denial assuming every earlier pending
-                // request allowed, whichever is longer. State in registers.
-                const uint64_t c_run = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-                SWGeo geo{};
-                uint64_t same_w = 0, elig_m = 0;
-                if constexpr (A != kAlgoTB) {
-                    if (pend) geo = sw_geo(q.now_ms, L);
-                    int64_t wmin = pend ? geo.curr_start : INT64_MAX;
-                    for (int o = 32; o > 0; o >>= 1) {
-                        const int64_t x = __shfl_xor(wmin, o, 64);
-                        wmin = x < wmin ? x : wmin;
-                    }
-                    const bool w0 = pend && geo.curr_start == wmin;
-                    same_w = __ballot(w0);
-                    elig_m = __ballot(w0 && q.op == (uint32_t)kOpAcquire);
-                }
-                uint64_t sa = S.sa[hs], sb = S.sb[hs], sc = S.sc[hs];
-                bool changed = false;
+            bool changed = false;
+            const uint64_t c_run = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+            if constexpr (A == kAlgoTB) {
+                // token bucket: rounds; each applies the prefix up to the first state change
+                // (every earlier pending request is denied and leaves the state alone, Lua
+                // :61-67), so a chunk costs 1 + its allows (the balance is a sequential fp64
+                // recurrence, Lua :56-63)
                 while (__any(pend)) {
-                    const uint64_t pm = __ballot(pend);
                     Outcome o{};
-                    SWAllow al{false, 0};
-                    bool elig = false;
-                    if (pend) {
-                        if constexpr (A == kAlgoTB) {
-                            o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
-                        } else {
-                            o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc);
-                            elig = (pm & ~(elig_m & same_w)) == 0 && (pm & (pm - 1)) != 0 &&
-                                   (int64_t)sa <= geo.curr_start;
-                            if (elig) al = sw_try_after_allows(L, q.permits, q.now_ms, geo, sa, sb, sc,
-                                                               popc_below(pm));
-                        }
-                    }
+                    if (pend) o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
                     const uint64_t mut = __ballot(pend && o.mutate);
                     const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
-                    uint32_t fa = 0;
-                    bool use_a = false;
-                    if constexpr (A != kAlgoTB) {
-                        const uint64_t den = __ballot(pend && elig && !al.allowed);
-                        fa = den ? (uint32_t)__builtin_ctzll(den) : 64u;
-                        use_a = __any(elig) && fa > fm;
+                    if (pend && lane <= fm) {
+                        oa = o.allowed;
+                        orem = o.remaining;
+                        tk = o.tokens;
+                        n_allowed += o.allowed ? 1u : 0u;
+                        pend = false;
                     }
-                    if (use_a) {
-                        if constexpr (A != kAlgoTB) {
-                            const uint64_t ok = pm & (fa >= 64u ? ~0ULL : ((1ULL << fa) - 1));
-                            const uint32_t last = 63u - (uint32_t)__builtin_clzll(ok);
-                            const int64_t t_last = __shfl(q.now_ms, (int)last, 64);
-                            SWGeo gl;                     // every lane commits the same state
-                            gl.curr_start = __shfl(geo.curr_start, (int)last, 64);
-                            gl.prev_start = __shfl(geo.prev_start, (int)last, 64);
-                            gl.prev_weight = __shfl(geo.prev_weight, (int)last, 64);
-                            sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)__popcll(ok), t_last);
-                            if (pend && lane <= fa) {
-                                oa = al.allowed;
-                                orem = al.remaining;
-                                n_allowed += al.allowed ? 1u : 0u;
-                                pend = false;
-                            }
+                    if (fm < 64u) {
+                        sa = __shfl(o.a, (int)fm, 64);
+                        sb = __shfl(o.b, (int)fm, 64);
+                        sc = __shfl(o.c, (int)fm, 64);
+                        changed = true;
+                    }
+                }
+            } else {
+                // sliding window: inside one window W the acquires only INCR the current
+                // bucket (:114-116), so with k allows before it a request's estimate is
+                // d2l(tv + (C0 + k)), tv = prev * pw at its own time (:174): the request is
+                // allowed iff k <= K, its largest such k. One pass computes tv and K per
+                // lane; the allows then follow by a greedy scan of integer compares (the
+                // k-th allow is the first request after the (k-1)-th with K >= k). Requests
+                // the scan cannot take (another window, before the newest bucket, a peek or
+                // a reset) run the exact step alone.
+                const SWGeo geo = pend ? sw_geo(q.now_ms, L) : SWGeo{};
+                const int64_t w = L.window_ms, mx = L.max_permits;
+                while (__any(pend)) {
+                    const uint32_t f0 = (uint32_t)__builtin_ctzll(__ballot(pend));
+                    const int64_t W0 = __shfl(geo.curr_start, (int)f0, 64);
+                    const bool scan = pend && q.op == (uint32_t)kOpAcquire && geo.curr_start == W0 &&
+                                      (int64_t)sa <= W0;
+                    const uint64_t und = __ballot(pend && !scan);
+                    const uint32_t stop = und ? (uint32_t)__builtin_ctzll(und) : 64u;
+                    const bool in = scan && lane < stop;
+                    if (__any(in)) {
+                        const SW2 s0 = sw_unpack(sa, sb, sc);
+                        const int64_t C0 = s0.b1_start == W0 ? (int64_t)s0.b1_cnt : 0;
+                        const int64_t P = in ? sw_get(s0, geo.prev_start, q.now_ms, w) : 0;
+                        const double tv = (double)P * geo.prev_weight;           // :174, rounded
+                        auto est = [&](int64_t k) { return d2l(tv + (double)(C0 + k)); };
+                        int64_t K = mx - (int64_t)q.permits - C0 - (int64_t)tv;  // ~ largest k
+                        if (K >= 0 && est(K) + q.permits > mx) --K;             // rounding edges
+                        if (K >= 0 && est(K) + q.permits > mx) --K;
+                        if (est(K + 1) + q.permits <= mx) ++K;
+                        if (K < -1) K = -1;
+                        // greedy scan: kk = allows before this request inside the chunk
+                        int64_t kk = 0, k = 0;
+                        bool al = false;
+                        uint32_t cur = 0, last = 0;
+                        for (;;) {
+                            const uint64_t m = __ballot(in && lane >= cur && K >= k);
+                            if (in && lane >= cur) kk = k;
+                            if (!m) break;
+                            const uint32_t fa = (uint32_t)__builtin_ctzll(m);
+                            if (lane == fa) al = true;
+                            last = fa;
+                            ++k;
+                            cur = fa + 1;
+                        }
+                        if (in) {
+                            const int64_t e = est(al ? kk + 1 : kk);             // after the request
+                            oa = al;
+                            orem = mx - e > 0 ? mx - e : 0;
+                            n_allowed += al ? 1u : 0u;
+                            pend = false;
+                        }
+                        if (k > 0) {
+                            const int64_t t_last = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
+                                (int)(uint32_t)(q.now_ms >> 32), (int)last) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q.now_ms, (int)last));
+                            SWGeo gl{};
+                            gl.curr_start = W0;
+                            sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)k, t_last);
                             changed = true;
                         }
-                    } else {
-                        if (pend && lane <= fm) {
+                    }
+                    if (stop < 64u) {
+                        // the exact step of request `stop` alone (wave-uniform arithmetic)
+                        const uint32_t op_s = (uint32_t)__builtin_amdgcn_readlane((int)q.op, (int)stop);
+                        const int32_t p_s = __builtin_amdgcn_readlane(q.permits, (int)stop);
+                        const int64_t t_s = __shfl(q.now_ms, (int)stop, 64);
+                        const Outcome o = sw_step_g(L, op_s, p_s, t_s, sw_geo(t_s, L), sa, sb, sc);
+                        if (lane == stop) {
                             oa = o.allowed;
                             orem = o.remaining;
-                            tk = o.tokens;
                             n_allowed += o.allowed ? 1u : 0u;
                             pend = false;
                         }
-                        if (fm < 64u) {
-                            sa = __shfl(o.a, (int)fm, 64);
-                            sb = __shfl(o.b, (int)fm, 64);
-                            sc = __shfl(o.c, (int)fm, 64);
+                        if (o.mutate) {
+                            sa = o.a; sb = o.b; sc = o.c;
                             changed = true;
                         }
                     }
                 }
+            }
+            if (changed) {
                 wave_fence();
                 if (lane == 0) { S.sa[hs] = sa; S.sb[hs] = sb; S.sc[hs] = sc; }
                 wave_fence();
-                // thresholds for the next chunks: search from this chunk's last hot request,
-                // unless the key changes state chunk after chunk (then no chunk could be
-                // skipped anyway: leave the range empty until a chunk without a change)
-                const uint64_t c_srch = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-                const bool dense = c == prev_detail + 1;
-                if (changed && dense) {
-                    T1 = T0;
-                    stale = true;
-                } else if (changed || stale) {
-                    const uint64_t hm = __ballot(hot);
-                    const int64_t from = __shfl(q.now_ms, 63 - __builtin_clzll(hm), 64);
-                    hot_thresholds<A>(L, sa, sb, sc, from, lo, hi, lane, &T0, &T1);
-                    stale = false;
-                }
-                if (a.dbg) {
-                    const uint64_t c_end = __builtin_amdgcn_s_memtime();
-                    cyc_run += c_srch - c_run;
-                    cyc_search += c_end - c_srch;
-                }
+                ++n_changed;
+            }
+            // [T0, T1) for the next chunks; none while the key changes state chunk after chunk
+            // (no chunk could be skipped anyway: recomputed after a chunk without a change)
+            const uint64_t c_srch = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+            const bool dense = c == prev_detail + 1;
+            if (changed && dense) {
+                T0 = hot_t0<A>(lo, hi, sa, sb, sc);
+                T1 = T0;
+                stale = true;
+            } else if (changed || stale) {
+                T0 = hot_t0<A>(lo, hi, sa, sb, sc);
+                T1 = hot_t1_lb<A>(L, sa, sb, sc, T0, hi);
+                ++n_tk;
+                stale = false;
+            }
+            if (a.dbg) {
+                const uint64_t c_end = __builtin_amdgcn_s_memtime();
+                cyc_run += c_srch - c_run;
+                cyc_search += c_end - c_srch;
             }
             if (hot) {
                 put_res<Res>(a, j, oa, orem);
@@ -1496,7 +1535,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 const uint64_t nsk = todo & ~__ballot(skip);
                 const uint32_t fst = nsk ? (uint32_t)__builtin_ctzll(nsk) : 64u;
                 if (((todo >> lane) & 1u) && lane < fst) {  // decided: the key's state is constant here
-                    sm[0] = S.sa[hs]; sm[1] = S.sb[hs]; sm[2] = S.sc[hs];
+                    sm[0] = sa; sm[1] = sb; sm[2] = sc;
                     sm[3] = (((v2 >> 24) & 0xFFu) << 8) | (ne ? 3u : 1u);
                 }
                 if (fst == 64u) break;
@@ -1526,7 +1565,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 const uint64_t nsk = todo & ~__ballot(skip);
                 const uint32_t fst = nsk ? (uint32_t)__builtin_ctzll(nsk) : 64u;
                 if (((todo >> lane) & 1u) && lane < fst) {  // a whole group decided
-                    sg[0] = S.sa[hs]; sg[1] = S.sb[hs]; sg[2] = S.sc[hs];
+                    sg[0] = sa; sg[1] = sb; sg[2] = sc;
                     sg[3] = (v3 & 0xFF00u) | (ne ? 3u : 1u);
                 }
                 if (fst == 64u) break;
@@ -1639,8 +1678,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             uint64_t* d = a.dbg + (size_t)region * kDbgWords;
             // top bit: a hot region; bits 0-31: detailed chunks, 32-62: other-key records
             d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = f.end - f.start;
-            d[3] = (uint64_t)n_detail | (s_w1[0] << 32) | (1ULL << 63);
-            d[4] = cyc_detail; d[5] = cyc_run; d[6] = cyc_search; d[7] = s_w1[1];
+            d[3] = (uint64_t)n_detail | (uint64_t)min(n_tk, 0xFFFFu) << 32 | (uint64_t)min(n_fb, 0x7FFFu) << 48 | (1ULL << 63);
+            d[4] = cyc_detail; d[5] = cyc_run; d[6] = cyc_search;
+            d[7] = min((uint64_t)n_changed, (uint64_t)0xFFFFFF);
         }
     }
 }
@@ -1648,8 +1688,11 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 // HOT: 2-wave workgroups; the first kHotMax run the hot regions' chains (hot_chain), the
 // rest two normal regions each: one launch, so the chains are dispatched before the
 // normal regions fill the machine, at the LDS per wave of the plain kernel.
+#ifndef RL_HOT_MIN_WAVES
+#define RL_HOT_MIN_WAVES 4
+#endif
 template <class Codec, class Res, bool TOK, int BS, bool HOT, bool CACHE = false>
-__global__ __launch_bounds__(HOT ? 128 : 64, HOT ? 4 : 1) void k_regions(RegionArgs a) {
+__global__ __launch_bounds__(HOT ? 128 : 64, HOT ? RL_HOT_MIN_WAVES : 1) void k_regions(RegionArgs a) {
     if constexpr (CACHE) {                       // some limiter keeps a local cache (BS 0, no hot path)
         __shared__ RegionTableX S;
         region_body_t<Codec, Res, TOK, 0>(a, blockIdx.x, S);

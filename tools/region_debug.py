@@ -47,7 +47,16 @@ for b in range(args.batches):
     eng.sync()
     st = eng.stage_times()
     d = eng.debug_region_times(nb)
-    d = d[d[:, 1] > 0]
+    idx = np.nonzero(d[:, 1] > 0)[0]
+    d = d[idx]
+    # limiter of each region: limiters own consecutive power-of-two region ranges
+    bases, acc = [], 0
+    for _ in cfg["limiters"]:
+        regions = -(-max(cfg["capacity"] * 2, rl_amd.REGION_SLOTS) // rl_amd.REGION_SLOTS)
+        k = max((regions - 1).bit_length(), 3)
+        bases.append(acc)
+        acc += 1 << k
+    lim_of = np.searchsorted(np.array(bases), idx, side="right") - 1
     t0 = d[:, 0].min()
     dur = (d[:, 1] - d[:, 0]) / 100.0          # us
     hot = (d[:, 3] >> np.uint64(63)) == 1
@@ -57,13 +66,16 @@ for b in range(args.batches):
     order = np.argsort(-dur)[:12]
     for i in order:
         rr = int(rounds[i])
-        cyc = " ".join(f"{x / 1e6:6.2f}" for x in d[i, 4:8])
-        what = (f"detail {rr & 0xFFFFFFFF:7d} (other keys {rr >> 32:7d}) HOT Mcyc det/run/srch/p2 {cyc}"
+        cyc = " ".join(f"{x / 1e6:6.2f}" for x in d[i, 4:7])
+        w7 = int(d[i, 7])
+        what = (f"detail {rr & 0xFFFFFFFF:7d} changed {w7 & 0xFFFFFF:6d} "
+                f"T1 updates {(rr >> 32) & 0xFFFF:6d} HOT Mcyc det/run/T1 {cyc}"
                 if hot[i] else f"rounds {rr:8d}")
-        print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  recs {int(d[i, 2]):9d} {what}")
+        print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  lim {lim_of[i]} "
+              f"recs {int(d[i, 2]):9d} {what}")
     nh = ~hot
     ends = (d[nh, 1] - t0) / 100
-    for q in (0.5, 0.9, 0.99, 0.999, 1.0):
+    for q in ((0.5, 0.9, 0.99, 0.999, 1.0) if nh.any() else ()):
         print(f"   normal regions end quantile {q}: {np.quantile(ends, q):9.1f} us")
     print(f"   normal: sum dur {dur[nh].sum() / 1e3:.1f} ms, recs {int(d[nh, 2].sum())}, "
           f"rounds {int(rounds[nh].sum())}")
