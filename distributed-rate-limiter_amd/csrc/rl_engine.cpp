@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <utility>
 #include <vector>
 
 #include "../../include/rl_engine.h"
@@ -107,6 +108,7 @@ struct rl_engine {
     uint8_t* s_allowed = nullptr;
     int64_t* s_remaining = nullptr;
     double* s_tokens = nullptr;
+    std::vector<std::pair<void*, size_t>> pinned;   // caller buffers registered by rl_pin_host
 
     // routing scratch
     uint32_t* route_scratch = nullptr;
@@ -248,6 +250,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
     dfree(e->route_scratch); dfree(e->route_counts); dfree(e->d_dir);
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
+    for (auto& pb : e->pinned) (void)hipHostUnregister(pb.first);
     for (int r = 0; r < kEvRing; ++r)
         for (int i = 0; i < kMarks; ++i) if (e->ev[r][i]) (void)hipEventDestroy(e->ev[r][i]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -669,6 +672,43 @@ extern "C" int rl_execute_batch(rl_engine* e, size_t n, const uint64_t* key,
     if (tokens_after) HIP_OK(hipMemcpyAsync(tokens_after, e->s_tokens, n * 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     return rc;
+}
+
+// Page-lock a caller's host buffer so the host-buffer entry points DMA it directly instead
+// of staging it through the runtime's bounce buffers (pageable memory). Registering an
+// already page-locked range (hipHostMalloc, another registration) is a no-op.
+extern "C" int rl_pin_host(rl_engine* e, void* ptr, size_t bytes) {
+    if (!e || !ptr || bytes == 0) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    for (auto& pb : e->pinned)
+        if (pb.first == ptr) return pb.second >= bytes ? RL_OK : RL_E_INVALID_ARG;
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, ptr) == hipSuccess && at.type == hipMemoryTypeHost) {
+        (void)hipGetLastError();
+        return RL_OK;                               // already page-locked by its owner
+    }
+    (void)hipGetLastError();
+    if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return RL_E_DEVICE;
+    }
+    e->pinned.emplace_back(ptr, bytes);
+    return RL_OK;
+}
+
+// Undo rl_pin_host; must be called before the caller frees the buffer. Unknown pointers
+// (never pinned by this engine) return RL_E_INVALID_ARG.
+extern "C" int rl_unpin_host(rl_engine* e, void* ptr) {
+    if (!e || !ptr) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    for (size_t i = 0; i < e->pinned.size(); ++i) {
+        if (e->pinned[i].first != ptr) continue;
+        (void)hipStreamSynchronize(e->stream);     // no copy of it in flight
+        const hipError_t r = hipHostUnregister(ptr);
+        e->pinned.erase(e->pinned.begin() + (long)i);
+        return r == hipSuccess ? RL_OK : RL_E_DEVICE;
+    }
+    return RL_E_INVALID_ARG;
 }
 
 extern "C" int rl_try_acquire_batch(rl_engine* e, size_t n, const uint64_t* key_hash,

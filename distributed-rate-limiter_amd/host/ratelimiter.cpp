@@ -80,7 +80,30 @@ GpuRateLimiter::GpuRateLimiter(std::shared_ptr<GpuEngine> engine, Algorithm algo
     id_ = engine_->addLimiter((int)algo, cfg_);
 }
 
-GpuRateLimiter::~GpuRateLimiter() = default;
+GpuRateLimiter::~GpuRateLimiter() { unpinFlush(); }
+
+void GpuRateLimiter::unpinFlush() {
+    if (fb_.cap == 0) return;
+    engine_->unpin(fb_.key.data()); engine_->unpin(fb_.permits.data());
+    engine_->unpin(fb_.now.data()); engine_->unpin(fb_.remaining.data());
+    engine_->unpin(fb_.lim.data()); engine_->unpin(fb_.op.data()); engine_->unpin(fb_.allowed.data());
+}
+
+// Grow the flush buffers (doubling) and page-lock them once, so every later flush DMAs
+// them directly (no pageable staging).
+void GpuRateLimiter::reserveFlush(size_t n) {
+    if (n <= fb_.cap) return;
+    unpinFlush();
+    size_t c = fb_.cap ? fb_.cap : 256;
+    while (c < n) c *= 2;
+    fb_.key.assign(c, 0); fb_.permits.assign(c, 0); fb_.now.assign(c, 0);
+    fb_.remaining.assign(c, 0); fb_.lim.assign(c, id_); fb_.op.assign(c, 0); fb_.allowed.assign(c, 0);
+    fb_.cap = c;
+    engine_->pin(fb_.key.data(), c * 8); engine_->pin(fb_.permits.data(), c * 4);
+    engine_->pin(fb_.now.data(), c * 8); engine_->pin(fb_.remaining.data(), c * 8);
+    engine_->pin(fb_.lim.data(), c * 2); engine_->pin(fb_.op.data(), c);
+    engine_->pin(fb_.allowed.data(), c);
+}
 
 void GpuRateLimiter::checkStatus(int st, const char* where) {
     if (st == RL_OK || st == RL_E_INVALID_REQUEST) return;
@@ -122,17 +145,19 @@ void GpuRateLimiter::flushLocked(std::unique_lock<std::mutex>& lk) {
     batch.swap(queue_);
     lk.unlock();
     const size_t n = batch.size();
-    std::vector<uint64_t> k(n);
-    std::vector<int32_t> pm(n);
-    std::vector<int64_t> t(n), rem(n);
-    std::vector<uint16_t> lim(n, id_);
-    std::vector<uint8_t> op(n), al(n);
+    reserveFlush(n);                    // the flush slot (flushing_) owns fb_
+    uint64_t* k = fb_.key.data();
+    int32_t* pm = fb_.permits.data();
+    int64_t* t = fb_.now.data();
+    uint8_t* op = fb_.op.data();
     for (size_t i = 0; i < n; ++i) {
         k[i] = batch[i]->key; pm[i] = batch[i]->permits; t[i] = batch[i]->now; op[i] = batch[i]->op;
     }
     uint64_t hits = 0;
-    int st = engine_->executeBatch(n, k.data(), pm.data(), t.data(), lim.data(), op.data(), al.data(),
-                                   rem.data(), &hits);
+    int st = engine_->executeBatch(n, k, pm, t, fb_.lim.data(), op, fb_.allowed.data(),
+                                   fb_.remaining.data(), &hits);
+    const uint8_t* al = fb_.allowed.data();
+    const int64_t* rem = fb_.remaining.data();
     cacheHits.increment(hits);
     lk.lock();
     for (size_t i = 0; i < n; ++i) {

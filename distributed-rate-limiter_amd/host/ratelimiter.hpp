@@ -110,6 +110,10 @@ class GpuEngine {
     GpuEngine(const GpuEngine&) = delete;
     GpuEngine& operator=(const GpuEngine&) = delete;
     rl_engine* handle() const { return e_; }
+    // Page-lock a reused host buffer for the engine's DMA (rl_pin_host); best effort:
+    // an unpinned buffer still works through pageable staging.
+    void pin(void* p, size_t bytes) { if (p && bytes) (void)rl_pin_host(e_, p, bytes); }
+    void unpin(void* p) { if (p) (void)rl_unpin_host(e_, p); }
     uint16_t addLimiter(int algo, const RateLimitConfig& c);
     // Runs one host batch and returns its status and cache-hit count atomically with
     // respect to the other limiters sharing this engine.
@@ -179,6 +183,17 @@ class GpuRateLimiter : public RateLimiter {
     std::condition_variable cv_;
     std::vector<Pending*> queue_;
     bool flushing_ = false;
+    // flush buffers, reused across flushes and page-locked (owned by the flush slot)
+    struct FlushBufs {
+        size_t cap = 0;
+        std::vector<uint64_t> key;
+        std::vector<int32_t> permits;
+        std::vector<int64_t> now, remaining;
+        std::vector<uint16_t> lim;
+        std::vector<uint8_t> op, allowed;
+    } fb_;
+    void reserveFlush(size_t n);
+    void unpinFlush();
 };
 
 }  // namespace ratelimiter

@@ -45,7 +45,7 @@ EXPORTS = [
     "rl_sweep_expired", "rl_route_return_bytes", "rl_route_fold_return",
     "rl_route_unpack_return", "rl_route_partition_device", "rl_set_owner_directory",
     "rl_owner_of_engine", "rl_router_create", "rl_router_step", "rl_router_finish",
-    "rl_router_plan_directory", "rl_router_destroy",
+    "rl_router_plan_directory", "rl_router_destroy", "rl_pin_host", "rl_unpin_host",
 ]
 RCCL_EXPORTS = ["rl_rccl_unique_id", "rl_transport_rccl_create", "rl_transport_rccl_destroy"]
 STATE_SW_BUCKET, STATE_TB_BUCKET = 0, 1
@@ -162,6 +162,8 @@ def lib():
     L.rl_route_partition_device.argtypes = [vp, sz, vp, u32, vp, vp, sz, vp]
     L.rl_set_owner_directory.argtypes = [vp, sz, vp, vp]
     L.rl_owner_of_engine.argtypes = [vp, ctypes.c_uint64]
+    L.rl_pin_host.argtypes = [vp, vp, sz]
+    L.rl_unpin_host.argtypes = [vp, vp]
     L.rl_owner_of_engine.restype = u32
     _lib = L
     return L
@@ -280,6 +282,13 @@ class Engine:
         if st in (RL_E_DEVICE, RL_E_NOMEM, RL_E_TOO_LARGE):
             raise RlError(st, "rl_execute_batch")
         return allowed, remaining, tokens, st
+
+    def pin_host(self, arr) -> int:
+        """rl_pin_host on a numpy array reused across host batches (status code)."""
+        return self._L.rl_pin_host(self._h, _p(arr), arr.nbytes)
+
+    def unpin_host(self, arr) -> int:
+        return self._L.rl_unpin_host(self._h, _p(arr))
 
     def try_acquire_batch(self, keys, permits, now_ns, limiter=None):
         a, r, _, st = self.execute(keys, permits, now_ns, limiter, None, want_tokens=False)

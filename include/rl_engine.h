@@ -155,6 +155,14 @@ int  rl_try_acquire_batch(rl_engine* e, size_t n,
                           const int64_t* now_ns, const uint16_t* limiter,
                           uint8_t* allowed, int64_t* remaining, double* tokens_after);
 
+/* Page-lock (hipHostRegister) a caller-owned host buffer that is reused across batches,
+ * so the host-buffer entry points above and below DMA it directly instead of staging it
+ * through pageable bounce buffers (the JNI side pins its direct ByteBuffers once, see
+ * INTEGRATION.md). Already page-locked memory is accepted as is. rl_unpin_host must be
+ * called before the buffer is freed; rl_destroy unpins whatever is left. */
+int  rl_pin_host(rl_engine* e, void* ptr, size_t bytes);
+int  rl_unpin_host(rl_engine* e, void* ptr);
+
 /* Mixed operations (RL_OP_*) over host buffers; `op` may be NULL (all ACQUIRE). */
 int  rl_execute_batch(rl_engine* e, size_t n,
                       const uint64_t* key_hash, const int32_t* permits,

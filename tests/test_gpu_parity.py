@@ -357,3 +357,31 @@ def test_sw_local_cache_random(ttl):
         e2.execute(*(x[cuts[b]:cuts[b + 1]] for x in tr))
         tot += e2.stats()["cache_hits"]
     assert tot == hits
+
+
+def test_pinned_host_buffers_match_pageable():
+    """rl_pin_host: page-locked caller buffers give the same results as pageable ones, over
+    several batches that reuse the same buffers (the micro-batcher's pattern)."""
+    lims = [(rl_amd.TB, 50, 60_000, 10.0), (rl_amd.SW, 20, 1_000, 0.0)]
+    n = 50_000
+    bufs = dict(keys=np.zeros(n, np.uint64), permits=np.zeros(n, np.int32),
+                now=np.zeros(n, np.int64), lim=np.zeros(n, np.uint16))
+    e = engine(lims)
+    ref = engine(lims)
+    o = COracle(lims)
+    for b in bufs.values():
+        assert e.pin_host(b) == rl_amd.RL_OK
+        assert e.pin_host(b) == rl_amd.RL_OK          # idempotent
+    for it in range(3):
+        k, p, t, l, _ = trace(900 + it, n, 5_000, 2, 4_000)
+        t = t + it * 4_000 * NS
+        bufs["keys"][:] = k; bufs["permits"][:] = p; bufs["now"][:] = t; bufs["lim"][:] = l
+        got = e.execute(bufs["keys"], bufs["permits"], bufs["now"], bufs["lim"])
+        want = ref.execute(k, p, t, l)
+        assert_same(got, want[:3], f"pinned batch {it}")
+        oa, orem, ot, _ = o.run(k, p, t, l)
+        assert_same(got, (oa, orem, ot), f"pinned batch {it} vs oracle")
+    for b in bufs.values():
+        assert e.unpin_host(b) == rl_amd.RL_OK
+    assert e.unpin_host(bufs["keys"]) == rl_amd.RL_E_INVALID_ARG   # no longer pinned
+    o.close()
