@@ -50,6 +50,32 @@ inline int ceil_log2(uint64_t x) {
 
 }  // namespace
 
+// Per-batch scratch: the partition's records/positions, the [bin][tile] counts, the packed
+// results and the batch control block. Two sets, so that with RL_OPT_PIPELINE the partition
+// of batch k+1 (its own stream) can run while batch k's region stage still reads its set.
+struct BatchScratch {
+    size_t cap_n = 0;
+    bool cap_wide = false;
+    void* rec0 = nullptr;
+    void* rec1 = nullptr;
+    uint32_t* pos0 = nullptr;
+    uint32_t* pos1 = nullptr;
+    void* res = nullptr;
+    int64_t* ext = nullptr;                 // escaped remainders (kResEscape), like res
+    double* tok = nullptr;
+    uint32_t* counts = nullptr;             // [bins][tiles]
+    size_t counts_cap = 0;
+    uint32_t* bin_total = nullptr;          // [2^kMaxDigitBits]
+    uint32_t* bin_base = nullptr;           // [2^kMaxDigitBits]
+    uint32_t* region_count = nullptr;       // [P padded]
+    uint32_t* region_start = nullptr;
+    size_t region_cap = 0;
+    BatchCtl* d_ctl = nullptr;
+    hipEvent_t parted = nullptr;            // pipeline: partition done (partition stream)
+    hipEvent_t freed = nullptr;             // pipeline: last reader of the set done (engine stream)
+    bool used = false;                      // `freed` has been recorded
+};
+
 struct rl_engine {
     int device = 0;
     rl_opts opts{};
@@ -63,23 +89,15 @@ struct rl_engine {
     uint8_t* d_region_lim = nullptr;
     size_t region_lim_cap = 0;
 
-    // scratch (sized for opts.max_batch)
-    size_t cap_n = 0;
-    bool cap_wide = false;
-    void* rec0 = nullptr;
-    void* rec1 = nullptr;
-    uint32_t* pos0 = nullptr;
-    uint32_t* pos1 = nullptr;
-    void* res = nullptr;
-    int64_t* ext = nullptr;                 // escaped remainders (kResEscape), like res
-    double* tok = nullptr;
-    uint32_t* counts = nullptr;             // [bins][tiles]
-    size_t counts_cap = 0;
-    uint32_t* bin_total = nullptr;          // [4096]
-    uint32_t* bin_base = nullptr;           // [4096]
-    uint32_t* region_count = nullptr;       // [P padded]
-    uint32_t* region_start = nullptr;
-    size_t region_cap = 0;
+    // per-batch scratch (sized for opts.max_batch); sc[0] unless pipelined
+    BatchScratch sc[2];
+    int next_set = 0;
+    bool pipeline = false;                  // RL_OPT_PIPELINE
+    hipStream_t pstream = nullptr;          // partition stream (pipeline)
+    hipEvent_t in_ev = nullptr;             // pipeline: inputs ready on e->stream
+    hipStream_t hstream = nullptr;          // hot chains beside the normal regions
+    hipEvent_t hot_ev[2] = {};              // fork / join of hstream
+    bool split_hot = true;                  // rl_tune("split_hot"): 0 = one 2-wave launch
     // hot regions
     uint32_t* hot_list = nullptr;           // [kHotMax + 40]: list, k_hot_select's meta, total
     HotInfo* hot_info = nullptr;            // [kHotMax]
@@ -94,7 +112,6 @@ struct rl_engine {
     uint64_t* dbg = nullptr;                // rl_tune("debug_regions"): per-bin stamps
     size_t dbg_cap = 0;
     bool debug_regions = false;
-    BatchCtl* d_ctl = nullptr;
     unsigned long long* d_stats = nullptr;  // [kStatSlots][kStWords] sharded counters (zeroed)
     BatchCtl* h_ctl = nullptr;              // pinned copy of the last batch's ctl
 
@@ -129,6 +146,8 @@ struct rl_engine {
     int bin_shift = 0;                      // rl_tune("bin_shift"): 0 or 3 (regions per bin 1/8)
     uint32_t up_per_cu = 0, sc_per_cu = 0, un_per_cu = 0;   // rl_tune("*_per_cu"), 0 = default
     bool force_wide = false;                // rl_tune("wide_records"): 32-B records (any time span)
+    bool auto_grow = true;                  // !RL_OPT_FIXED_CAPACITY
+    uint64_t grows = 0;                     // region-count doublings done (rl_batch_stats)
 };
 
 #define HIP_OK(x)                                                      \
@@ -217,16 +236,38 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
         rl_destroy(e);
         return RL_E_DEVICE;
     }
+    if (hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->hot_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->hot_ev[1], hipEventDisableTiming) != hipSuccess) {
+        rl_destroy(e);
+        return RL_E_DEVICE;
+    }
     e->timing = (o.flags & RL_OPT_STAGE_TIMING) != 0;
     if (e->timing) ensure_events(e);
-    int rc = dalloc(&e->d_ctl, 1);
+    e->pipeline = (o.flags & RL_OPT_PIPELINE) != 0;
+    e->auto_grow = (o.flags & RL_OPT_FIXED_CAPACITY) == 0;
+    if (e->pipeline && hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess) {
+        rl_destroy(e);
+        return RL_E_DEVICE;
+    }
+    int rc = RL_OK;
+    if (e->pipeline && hipEventCreateWithFlags(&e->in_ev, hipEventDisableTiming) != hipSuccess)
+        rc = RL_E_DEVICE;
+    for (int k = 0; k < (e->pipeline ? 2 : 1); ++k) {
+        BatchScratch& B = e->sc[k];
+        if (rc == RL_OK) rc = dalloc(&B.d_ctl, 1);
+        if (rc == RL_OK) rc = dalloc(&B.bin_total, 1u << kMaxDigitBits);
+        if (rc == RL_OK) rc = dalloc(&B.bin_base, 1u << kMaxDigitBits);
+        if (rc == RL_OK && e->pipeline &&
+            (hipEventCreateWithFlags(&B.parted, hipEventDisableTiming) != hipSuccess ||
+             hipEventCreateWithFlags(&B.freed, hipEventDisableTiming) != hipSuccess))
+            rc = RL_E_DEVICE;
+    }
     if (rc == RL_OK) rc = dalloc(&e->d_stats, (size_t)kStatSlots * kStWords);
     if (rc == RL_OK && hipMemset(e->d_stats, 0, (size_t)kStatSlots * kStWords * 8) != hipSuccess)
         rc = RL_E_DEVICE;
     if (rc == RL_OK && hipHostMalloc((void**)&e->h_ctl, sizeof(BatchCtl)) != hipSuccess) rc = RL_E_NOMEM;
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
-    if (rc == RL_OK) rc = dalloc(&e->bin_total, 1u << kMaxDigitBits);
-    if (rc == RL_OK) rc = dalloc(&e->bin_base, 1u << kMaxDigitBits);
     if (rc == RL_OK) rc = dalloc(&e->hot_list, kHotMax + 40);
     if (rc == RL_OK) rc = dalloc(&e->hot_info, kHotMax);
     if (rc != RL_OK) { rl_destroy(e); return rc; }
@@ -238,14 +279,21 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
 extern "C" void rl_destroy(rl_engine* e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->pstream) (void)hipStreamSynchronize(e->pstream);
+    if (e->hstream) (void)hipStreamSynchronize(e->hstream);
     for (auto& l : e->lims) { dfree(l.table); dfree(l.cache_table); }
     dfree(e->d_lims); dfree(e->d_region_lim);
-    dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
-    dfree(e->ext);
-    dfree(e->counts); dfree(e->bin_total); dfree(e->bin_base);
-    dfree(e->region_count); dfree(e->region_start);
+    for (BatchScratch& B : e->sc) {
+        dfree(B.rec0); dfree(B.rec1); dfree(B.pos0); dfree(B.pos1); dfree(B.res); dfree(B.tok);
+        dfree(B.ext);
+        dfree(B.counts); dfree(B.bin_total); dfree(B.bin_base);
+        dfree(B.region_count); dfree(B.region_start);
+        dfree(B.d_ctl);
+        if (B.parted) (void)hipEventDestroy(B.parted);
+        if (B.freed) (void)hipEventDestroy(B.freed);
+    }
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
-    dfree(e->d_ctl); dfree(e->d_stats);
+    dfree(e->d_stats);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
     dfree(e->route_scratch); dfree(e->route_counts); dfree(e->d_dir);
@@ -254,6 +302,10 @@ extern "C" void rl_destroy(rl_engine* e) {
     for (int r = 0; r < kEvRing; ++r)
         for (int i = 0; i < kMarks; ++i) if (e->ev[r][i]) (void)hipEventDestroy(e->ev[r][i]);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->pstream) (void)hipStreamDestroy(e->pstream);
+    if (e->in_ev) (void)hipEventDestroy(e->in_ev);
+    if (e->hstream) (void)hipStreamDestroy(e->hstream);
+    for (hipEvent_t ev : e->hot_ev) if (ev) (void)hipEventDestroy(ev);
     delete e;
 }
 
@@ -340,43 +392,105 @@ extern "C" int rl_add_limiter(rl_engine* e, int algo, int64_t max_permits, int64
     return rl_add_limiter_ex(e, &c, id);
 }
 
-static int ensure_scratch(rl_engine* e, size_t n, bool wide, uint32_t bins, uint32_t n_tiles) {
-    if (n > e->cap_n || (wide && !e->cap_wide)) {
+// Double limiter li's region count (k -> k + 1 region bits): new table, every old region
+// split in two by k_grow, old table freed, region ids of the later limiters shifted.
+// Synchronous; nothing may be in flight on the engine's streams.
+static int grow_once(rl_engine* e, size_t li) {
+    HostLimiter& h = e->lims[li];
+    DevLimiter& d = h.dev;
+    const int k = d.region_bits;
+    if (k + 1 + e->shard_bits > 40 || (uint64_t)e->n_regions + (1ULL << k) > (1ULL << 24))
+        return RL_E_LIMITERS;
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
+    const size_t nb = h.table_bytes * 2;
+    void* nt = nullptr;
+    void* nx = nullptr;
+    if (dalloc(&nt, nb) != RL_OK) return RL_E_NOMEM;
+    if (h.cache_table && dalloc(&nx, nb / sizeof(Slot) * sizeof(uint64_t)) != RL_OK) {
+        dfree(nt);
+        return RL_E_NOMEM;
+    }
+    if (launch_grow((const Slot*)h.table, (const uint64_t*)h.cache_table, (Slot*)nt, (uint64_t*)nx,
+                    1ULL << k, e->shard_bits, k + 1, d.algo, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess) {
+        dfree(nt); dfree(nx);
+        return RL_E_DEVICE;
+    }
+    dfree(h.table); dfree(h.cache_table);
+    h.table = nt; h.cache_table = nx; h.table_bytes = nb;
+    d.table = (uint64_t)(uintptr_t)nt;
+    d.cache_table = (uint64_t)(uintptr_t)nx;
+    d.region_bits = k + 1;
+    uint32_t base = 0;
+    for (auto& l : e->lims) { l.dev.region_base = base; base += 1u << l.dev.region_bits; }
+    e->n_regions = base;
+    ++e->grows;
+    return upload_limiters(e);
+}
+
+static int grow_to(rl_engine* e, size_t li, uint64_t min_keys) {
+    const uint64_t per_shard = (min_keys + e->opts.shard_count - 1) / e->opts.shard_count;
+    while ((e->lims[li].table_bytes / sizeof(Slot)) < per_shard * 2) {   // load <= 0.5
+        const int rc = grow_once(e, li);
+        if (rc != RL_OK) return rc;
+    }
+    return RL_OK;
+}
+
+extern "C" int rl_grow_limiter(rl_engine* e, uint16_t limiter, uint64_t min_keys) {
+    if (!e) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (limiter >= e->lims.size()) return RL_E_INVALID_ARG;
+    (void)hipSetDevice(e->device);
+    return grow_to(e, limiter, min_keys);
+}
+
+extern "C" int rl_limiter_slots(rl_engine* e, uint16_t limiter, uint64_t* slots) {
+    if (!e || !slots) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (limiter >= e->lims.size()) return RL_E_INVALID_ARG;
+    *slots = e->lims[limiter].table_bytes / sizeof(Slot);
+    return RL_OK;
+}
+
+static int ensure_scratch(rl_engine* e, BatchScratch& B, size_t n, bool wide, uint32_t bins, uint32_t n_tiles) {
+    if (n > B.cap_n || (wide && !B.cap_wide)) {
         size_t cap = std::max<size_t>(n, std::min<size_t>(e->opts.max_batch, std::max<size_t>(n, 1u << 20)));
         const size_t rb = wide ? sizeof(RecW) : sizeof(RecC);
         const size_t padn = cap + kTileThreads;   // kernels write inactive lanes past n
-        dfree(e->rec0); dfree(e->rec1); dfree(e->pos0); dfree(e->pos1); dfree(e->res); dfree(e->tok);
-        dfree(e->ext);
-        int rc = dalloc(&e->rec0, padn * rb);
-        if (rc == RL_OK) rc = dalloc(&e->rec1, padn * rb);
-        if (rc == RL_OK) rc = dalloc(&e->pos0, padn);
-        if (rc == RL_OK) rc = dalloc(&e->pos1, padn);
-        if (rc == RL_OK) rc = dalloc(&e->res, padn * sizeof(uint64_t));
-        if (rc == RL_OK) rc = dalloc(&e->tok, padn);
-        if (rc == RL_OK) rc = dalloc(&e->ext, padn);
-        if (rc != RL_OK) { e->cap_n = 0; return rc; }
-        e->cap_n = cap;
-        e->cap_wide = wide;
+        dfree(B.rec0); dfree(B.rec1); dfree(B.pos0); dfree(B.pos1); dfree(B.res); dfree(B.tok);
+        dfree(B.ext);
+        int rc = dalloc(&B.rec0, padn * rb);
+        if (rc == RL_OK) rc = dalloc(&B.rec1, padn * rb);
+        if (rc == RL_OK) rc = dalloc(&B.pos0, padn);
+        if (rc == RL_OK) rc = dalloc(&B.pos1, padn);
+        if (rc == RL_OK) rc = dalloc(&B.res, padn * sizeof(uint64_t));
+        if (rc == RL_OK) rc = dalloc(&B.tok, padn);
+        if (rc == RL_OK) rc = dalloc(&B.ext, padn);
+        if (rc != RL_OK) { B.cap_n = 0; return rc; }
+        B.cap_n = cap;
+        B.cap_wide = wide;
     }
     const size_t need_counts = (size_t)bins * n_tiles;
-    if (need_counts > e->counts_cap) {
-        dfree(e->counts);
+    if (need_counts > B.counts_cap) {
+        dfree(B.counts);
         size_t c = std::max(need_counts, (size_t)(1u << kMaxDigitBits) *
                                               ((std::max<size_t>(n, e->opts.max_batch) + kTile - 1) / kTile));
-        if (dalloc(&e->counts, c) != RL_OK) return RL_E_NOMEM;
-        e->counts_cap = c;
+        if (dalloc(&B.counts, c) != RL_OK) return RL_E_NOMEM;
+        B.counts_cap = c;
     }
     return RL_OK;
 }
 
 // rstart / rend per bin for two-pass partitions (k_bin_bounds).
-static int ensure_regions(rl_engine* e, size_t bins) {
-    if (bins <= e->region_cap) return RL_OK;
-    dfree(e->region_count); dfree(e->region_start);
-    int rc = dalloc(&e->region_count, bins);
-    if (rc == RL_OK) rc = dalloc(&e->region_start, bins);
-    if (rc != RL_OK) { e->region_cap = 0; return rc; }
-    e->region_cap = bins;
+static int ensure_regions(BatchScratch& B, size_t bins) {
+    if (bins <= B.region_cap) return RL_OK;
+    dfree(B.region_count); dfree(B.region_start);
+    int rc = dalloc(&B.region_count, bins);
+    if (rc == RL_OK) rc = dalloc(&B.region_start, bins);
+    if (rc != RL_OK) { B.region_cap = 0; return rc; }
+    B.region_cap = bins;
     return RL_OK;
 }
 
@@ -402,16 +516,17 @@ static int ensure_hot_mark(rl_engine* e, size_t bins) {
     return RL_OK;
 }
 
-static inline void mark_on(rl_engine* e, int i, hipStream_t st) {
+static inline void mark_on(rl_engine* e, hipStream_t st, int i) {
     if (e->timing) (void)hipEventRecord(e->ev[e->ring_next][i], st);
 }
-static inline void mark(rl_engine* e, int i) { mark_on(e, i, e->stream); }
+static inline void mark(rl_engine* e, int i) { mark_on(e, e->stream, i); }
 
 // The pipeline on device buffers, enqueued on e->stream. Returns an immediate status
 // (argument/launch errors); the data-dependent status is read back by rl_last_status.
 static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const int32_t* permits,
                             const int64_t* now_ns, const uint16_t* limiter, const uint8_t* op,
-                            uint8_t* allowed, int64_t* remaining, double* tokens_after) {
+                            uint8_t* allowed, int64_t* remaining, double* tokens_after,
+                            bool overlap = false) {
     if (n > e->opts.max_batch) return RL_E_TOO_LARGE;
     e->last_n = n;
     e->pending_status = false;
@@ -441,11 +556,34 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
     const int d0 = passes == 1 ? bitsP : bitsP - bitsP / 2;
     const int d1 = bitsP - d0;
-    int rc = ensure_scratch(e, n, wide, 1u << std::max(d0, d1), nt);
+    // Scratch set and partition stream. With RL_OPT_PIPELINE the partition (stages 1-3)
+    // runs on e->pstream into one of two scratch sets, so batch k+1's partition overlaps
+    // batch k's region stage; the region stage and the unpermute stay on e->stream (state
+    // updates in batch order). `overlap`: the caller guarantees the inputs are complete
+    // (device call with no stream); otherwise the partition first waits for everything
+    // enqueued on e->stream (inputs copied or produced there, or the caller's stream).
+    const int set = e->pipeline ? e->next_set : 0;
+    BatchScratch& B = e->sc[set];
+    hipStream_t ps = e->pipeline ? e->pstream : s;
+    const size_t need_counts = (size_t)(1u << std::max(d0, d1)) * nt;
+    if (e->pipeline && (n > B.cap_n || (wide && !B.cap_wide) || need_counts > B.counts_cap ||
+                        (passes == 2 && n_bins > B.region_cap))) {
+        // growing a set frees its old buffers: nothing may still be using them
+        HIP_OK(hipStreamSynchronize(s));
+        HIP_OK(hipStreamSynchronize(ps));
+    }
+    int rc = ensure_scratch(e, B, n, wide, 1u << std::max(d0, d1), nt);
     if (rc != RL_OK) return rc;
     if (passes == 2) {
-        rc = ensure_regions(e, n_bins);
+        rc = ensure_regions(B, n_bins);
         if (rc != RL_OK) return rc;
+    }
+    if (e->pipeline) {
+        if (B.used) HIP_OK(hipStreamWaitEvent(ps, B.freed, 0));    // the set's last batch is done
+        if (!overlap) {
+            HIP_OK(hipEventRecord(e->in_ev, s));
+            HIP_OK(hipStreamWaitEvent(ps, e->in_ev, 0));
+        }
     }
     // the hot-key path assumes that a denial never changes state; with a local cache a
     // denial may (it puts the estimate, SlidingWindowRateLimiter.java:106-108)
@@ -461,46 +599,46 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     e->last_wide = wide;
 
-    mark(e, 0);
+    mark_on(e, ps, 0);
     PartArgs pa{};
     pa.key = key; pa.permits = permits; pa.now_ns = now_ns; pa.limiter = limiter; pa.op = op;
     pa.n = (uint32_t)n; pa.n_tiles = nt; pa.n_lim = (uint32_t)e->lims.size();
-    pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = e->d_ctl;
-    pa.counts = e->counts; pa.bin_base = e->bin_base; pa.ablate = e->ablate;
+    pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = B.d_ctl;
+    pa.counts = B.counts; pa.bin_base = B.bin_base; pa.ablate = e->ablate;
     pa.bin_shift = bsh;
     pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu;
     // ---- pass 0 (low digit) from the caller's arrays
     pa.digit_shift = 0; pa.digit_bits = d0;
     pa.region_count = nullptr;
-    pa.rec_out = e->rec0; pa.pos_out = e->pos0;
-    HIP_OK(launch_upsweep(pa, true, wide, s));
-    mark(e, 1);
-    HIP_OK(launch_scan_rows(e->counts, e->counts, 1u << d0, nt, e->bin_total, s));
-    HIP_OK(launch_scan_small(e->bin_total, e->bin_base, 1u << d0, s));
-    mark(e, 2);
-    HIP_OK(launch_scatter(pa, true, wide, s));
-    mark(e, 3);
-    const void* rec_final = e->rec0;
-    const uint32_t* rstart = e->bin_base;
-    const uint32_t* rcount = e->bin_total;
+    pa.rec_out = B.rec0; pa.pos_out = B.pos0;
+    HIP_OK(launch_upsweep(pa, true, wide, ps));
+    mark_on(e, ps, 1);
+    HIP_OK(launch_scan_rows(B.counts, B.counts, 1u << d0, nt, B.bin_total, ps));
+    HIP_OK(launch_scan_small(B.bin_total, B.bin_base, 1u << d0, ps));
+    mark_on(e, ps, 2);
+    HIP_OK(launch_scatter(pa, true, wide, ps));
+    mark_on(e, ps, 3);
+    const void* rec_final = B.rec0;
+    const uint32_t* rstart = B.bin_base;
+    const uint32_t* rcount = B.bin_total;
     const uint32_t* rend = nullptr;
     if (passes == 2) {
         // ---- pass 1 (high digit) over the records; stable, so the final order is
         // bin-major and arrival-ordered inside each bin.
         pa.digit_shift = d0; pa.digit_bits = d1;
-        pa.rec_in = e->rec0; pa.rec_out = e->rec1; pa.pos_out = e->pos1;
-        HIP_OK(launch_upsweep(pa, false, wide, s));
-        mark(e, 4);
-        HIP_OK(launch_scan_rows(e->counts, e->counts, 1u << d1, nt, e->bin_total, s));
-        HIP_OK(launch_scan_small(e->bin_total, e->bin_base, 1u << d1, s));
-        mark(e, 5);
-        HIP_OK(launch_scatter(pa, false, wide, s));
-        rec_final = e->rec1;
+        pa.rec_in = B.rec0; pa.rec_out = B.rec1; pa.pos_out = B.pos1;
+        HIP_OK(launch_upsweep(pa, false, wide, ps));
+        mark_on(e, ps, 4);
+        HIP_OK(launch_scan_rows(B.counts, B.counts, 1u << d1, nt, B.bin_total, ps));
+        HIP_OK(launch_scan_small(B.bin_total, B.bin_base, 1u << d1, ps));
+        mark_on(e, ps, 5);
+        HIP_OK(launch_scatter(pa, false, wide, ps));
+        rec_final = B.rec1;
     } else {
-        mark(e, 4);
-        mark(e, 5);
+        mark_on(e, ps, 4);
+        mark_on(e, ps, 5);
     }
-    mark(e, 6);
+    mark_on(e, ps, 6);
     if (passes == 2) {
         // bin boundaries of the final order: binary searches inside the high-digit runs
         // that pass 1's scan delimits (no per-request atomics: a hot bin would serialise
@@ -508,19 +646,23 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         BoundsArgs ba{};
         ba.rec = rec_final; ba.n = (uint32_t)n; ba.n_lim = (uint32_t)e->lims.size();
         ba.lims = e->d_lims; ba.shard_bits = e->shard_bits; ba.bin_shift = bsh;
-        ba.rstart = e->region_start; ba.rend = e->region_count;
-        ba.hi_base = e->bin_base; ba.hi_total = e->bin_total;
+        ba.rstart = B.region_start; ba.rend = B.region_count;
+        ba.hi_base = B.bin_base; ba.hi_total = B.bin_total;
         ba.n_bins = n_bins; ba.d0 = d0; ba.d1 = d1;
-        HIP_OK(launch_bin_bounds(ba, wide, s));
-        rstart = e->region_start;
+        HIP_OK(launch_bin_bounds(ba, wide, ps));
+        rstart = B.region_start;
         rcount = nullptr;
-        rend = e->region_count;
+        rend = B.region_count;
+    }
+    if (e->pipeline) {
+        HIP_OK(hipEventRecord(B.parted, ps));
+        HIP_OK(hipStreamWaitEvent(s, B.parted, 0));
     }
     RegionArgs ra{};
     ra.rec = rec_final; ra.rstart = rstart; ra.rcount = rcount; ra.rend = rend;
     ra.region_lim = e->d_region_lim;
-    ra.lims = e->d_lims; ra.res = e->res; ra.ext = e->ext; ra.tok = tokens_after ? e->tok : nullptr;
-    ra.ctl = e->d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
+    ra.lims = e->d_lims; ra.res = B.res; ra.ext = B.ext; ra.tok = tokens_after ? B.tok : nullptr;
+    ra.ctl = B.d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
     ra.skew_ms = e->opts.max_skew_ms;
     ra.stats = e->d_stats;
@@ -547,17 +689,19 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
     }
     mark(e, 7);
-    HIP_OK(launch_region(ra, wide, res_bytes, s));       // hot chains first, then the regions
+    // hot chains first (side stream), then the regions
+    HIP_OK(launch_region(ra, wide, res_bytes, s, e->split_hot ? e->hstream : nullptr, e->hot_ev[0],
+                         e->hot_ev[1]));
     mark(e, 10);
     if (hot) HIP_OK(launch_hot_fill(ra, wide, res_bytes, s));
-    HIP_OK(launch_stats_reduce(e->d_stats, e->d_ctl, s));
+    HIP_OK(launch_stats_reduce(e->d_stats, B.d_ctl, s));
     mark(e, 11);
     mark(e, 8);
     UnpermArgs ua{};
-    ua.pos0 = e->pos0; ua.pos1 = passes == 2 ? e->pos1 : nullptr; ua.res = e->res;
-    ua.mid = e->rec0;                                    // pass-0 records are dead by now
-    ua.tok = tokens_after ? e->tok : nullptr;
-    ua.ext = e->ext; ua.ctl = e->d_ctl;
+    ua.pos0 = B.pos0; ua.pos1 = passes == 2 ? B.pos1 : nullptr; ua.res = B.res;
+    ua.mid = B.rec0;                                    // pass-0 records are dead by now
+    ua.tok = tokens_after ? B.tok : nullptr;
+    ua.ext = B.ext; ua.ctl = B.d_ctl;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
     ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate; ua.per_cu = e->un_per_cu;
     HIP_OK(launch_unpermute(ua, res_bytes, s));
@@ -566,13 +710,19 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         e->ring_next = (e->ring_next + 1) % kEvRing;
         e->ring_used = std::min(e->ring_used + 1, kEvRing);
     }
-    HIP_OK(hipMemcpyAsync(e->h_ctl, e->d_ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(e->h_ctl, B.d_ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, s));
+    if (e->pipeline) {
+        HIP_OK(hipEventRecord(B.freed, s));
+        B.used = true;
+        e->next_set ^= 1;
+    }
     e->pending_status = true;
     return RL_OK;
 }
 
 static int collect_status(rl_engine* e) {
     HIP_OK(hipStreamSynchronize(e->stream));
+    if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
     if (!e->pending_status) return e->last_status;
     e->pending_status = false;
     const BatchCtl& c = *e->h_ctl;
@@ -581,6 +731,16 @@ static int collect_status(rl_engine* e) {
     if (c.cap_err) st = RL_E_CAPACITY;
     if (c.span_overflow) st = RL_E_INVALID_ARG;
     e->last_status = st;
+    // on-demand growth: a limiter whose regions are filling up (or overflowed: then twice)
+    // gets twice (four times) the regions before the next batch
+    if (e->auto_grow && (c.grow[0] | c.grow[1] | c.grow[2] | c.grow[3])) {
+        for (size_t li = 0; li < e->lims.size(); ++li) {
+            if (!((c.grow[li >> 6] >> (li & 63)) & 1ULL)) continue;
+            for (int t = 0; t < (c.cap_err ? 2 : 1); ++t)
+                if (grow_once(e, li) != RL_OK) break;      // at the table-size limit: stay
+        }
+        e->h_ctl->grow[0] = e->h_ctl->grow[1] = e->h_ctl->grow[2] = e->h_ctl->grow[3] = 0;
+    }
     return st;
 }
 
@@ -607,7 +767,7 @@ extern "C" int rl_execute_batch_device(rl_engine* e, size_t n, const uint64_t* k
         return rc;
     }
     return run_batch_device(e, n, key, permits, now_ns, limiter, op, allowed, remaining,
-                            tokens_after);
+                            tokens_after, /*overlap=*/user == nullptr);
 }
 
 extern "C" int rl_last_status(rl_engine* e) {
@@ -756,8 +916,9 @@ extern "C" int rl_batch_stats_get(rl_engine* e, rl_batch_stats* out) {
     out->invalid = c.invalid;
     out->capacity_errors = c.cap_err;
     out->regions_touched = c.regions;
-    out->table_bytes = c.regions * (uint64_t)kRegionSlots * sizeof(Slot) * 2;
+    out->table_bytes = c.table_bytes;
     out->cache_hits = c.cache_hits;
+    out->table_grows = e->grows;
     return RL_OK;
 }
 
@@ -810,6 +971,10 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
         e->sparse_max = (uint32_t)value;
         return RL_OK;
     }
+    if (std::strcmp(key, "split_hot") == 0) {
+        e->split_hot = value != 0;
+        return RL_OK;
+    }
     if (std::strcmp(key, "bin_shift") == 0) {
         if (value != 0 && value != kBinShift) return RL_E_INVALID_ARG;
         e->bin_shift = (int)value;
@@ -821,6 +986,7 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
 extern "C" int rl_sync(rl_engine* e) {
     if (!e) return RL_E_INVALID_ARG;
     HIP_OK(hipStreamSynchronize(e->stream));
+    if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
     return RL_OK;
 }
 

@@ -217,6 +217,8 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
             c->span_overflow = 0;
             c->n_esc = 0;
             c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = c->cache_hits = 0;
+            c->grow[0] = c->grow[1] = c->grow[2] = c->grow[3] = 0;
+            c->table_bytes = 0;
         }
     }
     const uint32_t mask = bins - 1;
@@ -539,8 +541,18 @@ __device__ inline void put_res(const RegionArgs& a, uint32_t j, bool alw, int64_
     }
 }
 
+// Growth signal of a region after its batch (lane 0): `used` live keys, or an overflow.
+__device__ inline void note_fill(const RegionArgs& a, uint32_t region, uint32_t used, bool overflow) {
+    if (used > kGrowUsed || overflow) {
+        const uint32_t li = a.region_lim[region];
+        atomicOr(&a.ctl->grow[li >> 6], 1ULL << (li & 63));
+    }
+}
+
 // Apply one group of up to 64 requests (lane order = arrival order; `valid` lanes only).
-template <class Codec, int ALGO, class LdsT>
+// SP: the region may be sparse (unloaded buckets, tombstones); image regions (SP = false)
+// compile those checks out of the probe loop.
+template <class Codec, int ALGO, bool SP, class LdsT>
 __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimiter& L,
                                      uint32_t lane, const typename Codec::Rec& cur, bool valid,
                                      uint32_t j, int64_t base, uint32_t pad, uint32_t& n_allowed,
@@ -575,7 +587,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             uint32_t p = home, tomb = kNone;
             for (uint32_t step = 0; step < NS / 4; ++step) {
                 const uint4 o4 = *(const uint4*)&S.occ[p];
-                if (kSparseOn && (o4.x & kOccUnloaded)) {  // a bucket is loaded whole
+                if (SP && (o4.x & kOccUnloaded)) {  // a bucket is loaded whole
                     fault = p;
                     sp.long_chain |= step >= 2;
                     break;
@@ -584,7 +596,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 const ulonglong2 t23 = *(const ulonglong2*)&S.tag[p + 2];
                 const uint32_t occm = (o4.x & 1u) | (o4.y & 1u) << 1 | (o4.z & 1u) << 2 |
                                       (o4.w & 1u) << 3;
-                const uint32_t tombm = !kSparseOn ? 0u : (o4.x >> 3 & 1u) | (o4.y >> 3 & 1u) << 1 |
+                const uint32_t tombm = !SP ? 0u : (o4.x >> 3 & 1u) | (o4.y >> 3 & 1u) << 1 |
                                                          (o4.z >> 3 & 1u) << 2 | (o4.w >> 3 & 1u) << 3;
                 const uint32_t hit = occm & ~tombm &
                                      ((t01.x == q.h ? 1u : 0u) | (t01.y == q.h ? 2u : 0u) |
@@ -609,7 +621,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 else { need = false; failed = true; }
             }
         }
-        if (kSparseOn && __any(fault != kNone)) {
+        if (SP && __any(fault != kNone)) {
             // lanes faulting the same bucket write the same words; nothing else in the
             // wave touches an unloaded bucket
             if (fault != kNone) fault_bucket(sp, L, S, fault);
@@ -825,13 +837,14 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     uint32_t head = 0, count = 0;                    // ring state (wave-uniform)
     // the whole stream is instantiated once per algorithm (uniform per region), so the
     // compiler hoists nothing of the other algorithm into the hot loop
-    auto stream = [&](auto algo) {
+    auto stream = [&](auto algo, auto spc) {
         constexpr int A = decltype(algo)::value;
+        constexpr bool SPX = decltype(spc)::value;
         auto slice = [&](const Rec& r, uint32_t c0) {
             const uint32_t idx = c0 + lane;
             if constexpr (RPB == 1) {
                 // the bin is the region: every record is ours, applied straight from registers
-                const Applied ap = wave_apply<Codec, A>(a, S, L, lane, r, idx < end, idx, base, pad,
+                const Applied ap = wave_apply<Codec, A, SPX>(a, S, L, lane, r, idx < end, idx, base, pad,
                                                      n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
@@ -850,7 +863,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
                 ap.j = pad; ap.alw = false; ap.rem = kRemError; ap.tok = 0.0;
                 if (count >= 64) {
                     const uint32_t ri = (head + lane) % kRing;
-                    ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
+                    ap = wave_apply<Codec, A, SPX>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
                                            n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
                     head = (head + 64) % kRing;
                     count -= 64;
@@ -878,15 +891,22 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
             if (count > 0) {
                 const bool v = lane < count;
                 const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
-                const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
+                const Applied ap = wave_apply<Codec, A, SPX>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
                                                      pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
         }
     };
-    if (L.algo == kAlgoTB) stream(std::integral_constant<int, kAlgoTB>{});
-    else stream(std::integral_constant<int, kAlgoSW>{});
+    using SpOn = std::integral_constant<bool, kSparseOn && RPB == 1>;
+    using SpOff = std::integral_constant<bool, false>;
+    if (L.algo == kAlgoTB) {
+        if (sparse) stream(std::integral_constant<int, kAlgoTB>{}, SpOn{});
+        else stream(std::integral_constant<int, kAlgoTB>{}, SpOff{});
+    } else {
+        if (sparse) stream(std::integral_constant<int, kAlgoSW>{}, SpOn{});
+        else stream(std::integral_constant<int, kAlgoSW>{}, SpOff{});
+    }
     wave_fence();
     uint32_t touched = 0;
     for (uint32_t s = lane; s < NS; s += 64) touched += (S.occ[s] & kOccTouched) ? 1u : 0u;
@@ -915,8 +935,14 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     }
     // ---- write the region back: every slot (free ones as zeros), or in a sparse region
     // only the slots this batch touched
+    uint32_t used = 0;                               // live keys (whole regions only)
+    uint32_t moved = 0;                              // table bytes read + written (sparse)
+    const uint32_t xw = xtab ? 8u : 0u;              // local-cache word per slot
     for (uint32_t s = lane; s < NS; s += 64) {
         const uint32_t o = S.occ[s];
+        used += (whole && (o & kOccUsed) && !(o & kOccTomb)) ? 1u : 0u;
+        if (!whole) moved += (!(o & kOccUnloaded) && (s & 3u) == 0 ? 4u * (32u + xw) : 0u) +
+                             ((o & kOccTouched) ? 32u + xw : 0u);
         if (!whole && !(o & kOccTouched)) continue;
         Slot v{0, 0, 0, 0};
         uint64_t x = 0;
@@ -934,9 +960,14 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         n_caperr += __shfl_xor(n_caperr, off, 64);
         n_hits += __shfl_xor(n_hits, off, 64);
         touched += __shfl_xor(touched, off, 64);
+        used += __shfl_xor(used, off, 64);
+        moved += __shfl_xor(moved, off, 64);
     }
     if (lane == 0) {
+        note_fill(a, region, used, n_caperr != 0);
         unsigned long long* st = a.stats + (size_t)(blockIdx.x & (kStatSlots - 1)) * kStWords;
+        atomicAdd(st + kStTableBytes, whole ? (unsigned long long)(2u * NS * (32u + xw))
+                                            : (unsigned long long)moved);
         if (n_allowed) atomicAdd(st + kStAllowed, (unsigned long long)n_allowed);
         if (n_invalid) atomicAdd(st + kStInvalid, (unsigned long long)n_invalid);
         if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
@@ -1583,7 +1614,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             const bool v = lane < valid_n;
             const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
             uint32_t n_hits = 0;                          // (no local cache on the hot path)
-            const Applied ap = wave_apply<Codec, A>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
+            const Applied ap = wave_apply<Codec, A, false>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
             if (v) {
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
@@ -1661,19 +1692,25 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     if (wid != 0) return;
     if (lane == 0 && hot_ok && touched_hot) S.occ[hs] |= 2u;
     wave_fence();
-    uint32_t touched = 0;
+    uint32_t touched = 0, used = 0;
     for (uint32_t sl = lane; sl < NS; sl += 64) {
         const uint32_t o = S.occ[sl];
         Slot v{0, 0, 0, 0};
         if (o & kOccUsed) v = slot_used(Slot{S.tag[sl], S.sa[sl], S.sb[sl], S.sc[sl]});
         tab[sl] = v;
         touched += (o >> 1) & 1u;
+        used += o & kOccUsed;
     }
-    for (int off = 32; off > 0; off >>= 1) touched += __shfl_xor(touched, off, 64);
+    for (int off = 32; off > 0; off >>= 1) {
+        touched += __shfl_xor(touched, off, 64);
+        used += __shfl_xor(used, off, 64);
+    }
     if (lane == 0) {
+        note_fill(a, region, used, n_caperr != 0);
         unsigned long long* st = a.stats + (size_t)(blockIdx.x & (kStatSlots - 1)) * kStWords;
         atomicAdd(st + kStDistinct, (unsigned long long)touched);
         atomicAdd(st + kStRegions, 1ULL);
+        atomicAdd(st + kStTableBytes, (unsigned long long)(2u * NS * 32u));
         if (a.dbg) {
             uint64_t* d = a.dbg + (size_t)region * kDbgWords;
             // top bit: a hot region; bits 0-31: detailed chunks, 32-62: other-key records
@@ -1691,8 +1728,12 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 #ifndef RL_HOT_MIN_WAVES
 #define RL_HOT_MIN_WAVES 4
 #endif
+// Normal regions (one wave each) at >= RL_REGION_MIN_WAVES waves per SIMD (VGPR budget).
+#ifndef RL_REGION_MIN_WAVES
+#define RL_REGION_MIN_WAVES 4
+#endif
 template <class Codec, class Res, bool TOK, int BS, bool HOT, bool CACHE = false>
-__global__ __launch_bounds__(HOT ? 128 : 64, HOT ? RL_HOT_MIN_WAVES : 1) void k_regions(RegionArgs a) {
+__global__ __launch_bounds__(HOT ? 128 : 64, HOT ? RL_HOT_MIN_WAVES : RL_REGION_MIN_WAVES) void k_regions(RegionArgs a) {
     if constexpr (CACHE) {                       // some limiter keeps a local cache (BS 0, no hot path)
         __shared__ RegionTableX S;
         region_body_t<Codec, Res, TOK, 0>(a, blockIdx.x, S);
@@ -1708,6 +1749,15 @@ __global__ __launch_bounds__(HOT ? 128 : 64, HOT ? RL_HOT_MIN_WAVES : 1) void k_
         __shared__ RegionLds<Codec, (BS > 0)> S;
         region_body_t<Codec, Res, TOK, BS>(a, blockIdx.x, S);
     }
+}
+
+// The hot chains alone (2-wave workgroups), launched on a side stream just before the
+// normal regions' single-wave launch: no normal region waits for the other region of a
+// 2-wave workgroup, and the chains still start first.
+template <class Codec, class Res, bool TOK>
+__global__ __launch_bounds__(128, RL_HOT_MIN_WAVES) void k_hot_chains(RegionArgs a) {
+    __shared__ RegionLds<Codec, true> S;
+    hot_chain<Codec, Res, TOK>(a, blockIdx.x, S);
 }
 
 // Phase C (one wave per chunk, all CUs): results of the chunks the chain decided.
@@ -2506,6 +2556,52 @@ __global__ __launch_bounds__(64) void k_import(ImportArgs a) {
     write_region(S, tab, xt, lane);
 }
 
+// Table growth (rl_grow_limiter): old region r of a limiter with 2^(k_new-1) regions splits
+// into new regions 2r and 2r+1 by the next tag bit (region_local with one more bit); every
+// slot holding state keeps its words and is re-inserted from its home in its new region.
+// One wave per old region; each new region is written whole (free slots as zeros).
+__global__ __launch_bounds__(64) void k_grow(const Slot* __restrict__ old_tab, const uint64_t* old_x,
+                                             Slot* __restrict__ new_tab, uint64_t* new_x,
+                                             uint64_t n_old, int shard_bits, int k_new, int algo) {
+    __shared__ RegionStage S[2];
+    constexpr uint32_t NS = kRegionSlots;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t r = blockIdx.x;
+    if (r >= n_old) return;
+    Slot img[NS / 64];
+    uint64_t xim[NS / 64];
+    bool kp[NS / 64];
+#pragma unroll
+    for (uint32_t i = 0; i < NS / 64; ++i) {
+        img[i] = old_tab[r * NS + lane + 64 * i];
+        xim[i] = old_x ? old_x[r * NS + lane + 64 * i] : 0;
+        kp[i] = !slot_free(img[i], xim[i]) && (xim[i] != 0 || state_present(algo, img[i].b, img[i].c));
+        S[0].occ[lane + 64 * i] = 0;
+        S[1].occ[lane + 64 * i] = 0;
+    }
+    wave_fence();
+#pragma unroll
+    for (uint32_t i = 0; i < NS / 64; ++i) {
+        if (!kp[i]) continue;
+        RegionStage& T = S[region_local(img[i].tag, shard_bits, k_new) & 1u];
+        uint32_t p = slot_home(img[i].tag);
+        while (atomicCAS(&T.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+        T.tag[p] = img[i].tag; T.sa[p] = img[i].a; T.sb[p] = img[i].b; T.sc[p] = img[i].c;
+        T.sx[p] = xim[i];
+    }
+    wave_fence();
+    write_region(S[0], new_tab + (2 * r) * NS, new_x ? new_x + (2 * r) * NS : nullptr, lane);
+    write_region(S[1], new_tab + (2 * r + 1) * NS, new_x ? new_x + (2 * r + 1) * NS : nullptr, lane);
+}
+
+hipError_t launch_grow(const Slot* old_tab, const uint64_t* old_x, Slot* new_tab, uint64_t* new_x,
+                       uint64_t n_old_regions, int shard_bits, int k_new, int algo, hipStream_t s) {
+    if (n_old_regions == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_grow, dim3((uint32_t)n_old_regions), dim3(64), 0, s, old_tab, old_x, new_tab,
+                       new_x, n_old_regions, shard_bits, k_new, algo);
+    return hipGetLastError();
+}
+
 // TTL sweep: one wave per region; every used slot none of whose buckets is live at `now`
 // (slot_live, the criterion a batch's region load applies) is dropped and the region is
 // rebuilt (no tombstone survives a sweep). One counter atomic per wave.
@@ -2604,9 +2700,20 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
 }
 
 template <class Codec, class Res>
-static void region_launch(const RegionArgs& a, hipStream_t s) {
+static void region_launch(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0,
+                          hipEvent_t e1) {
     const dim3 b(64);
-    if (a.bin_shift == 0 && a.hot_mark) {                // hot chains + normal regions
+    if (a.bin_shift == 0 && a.hot_mark && hs) {          // hot chains beside normal regions
+        (void)hipEventRecord(e0, s);
+        (void)hipStreamWaitEvent(hs, e0, 0);
+        if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true>), dim3(kHotMax), dim3(128), 0, hs, a);
+        else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false>), dim3(kHotMax), dim3(128), 0, hs, a);
+        const dim3 g(a.n_regions);
+        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0, false>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0, false>), g, b, 0, s, a);
+        (void)hipEventRecord(e1, hs);
+        (void)hipStreamWaitEvent(s, e1, 0);
+    } else if (a.bin_shift == 0 && a.hot_mark) {         // hot chains + normal regions
         const dim3 g(kHotMax + (a.n_regions + 1) / 2), b2(128);
         if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, 0, true>), g, b2, 0, s, a);
         else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0, true>), g, b2, 0, s, a);
@@ -2647,7 +2754,8 @@ __global__ __launch_bounds__(256) void k_stats_reduce(unsigned long long* stats,
         const unsigned long long v = part[t][0] + part[t][1] + part[t][2] + part[t][3];
         unsigned long long* dst = t == kStAllowed ? &ctl->allowed : t == kStInvalid ? &ctl->invalid
                                 : t == kStCapErr ? &ctl->cap_err : t == kStDistinct ? &ctl->distinct
-                                : t == kStRegions ? &ctl->regions : &ctl->cache_hits;
+                                : t == kStRegions ? &ctl->regions : t == kStCacheHits ? &ctl->cache_hits
+                                : &ctl->table_bytes;
         *dst += v;
     }
 }
@@ -2657,11 +2765,12 @@ hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStre
     return hipGetLastError();
 }
 
-hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
-    if (wide) region_launch<CodecW, uint64_t>(a, s);
-    else if (res_bytes == 1) region_launch<CodecC, uint8_t>(a, s);
-    else if (res_bytes == 2) region_launch<CodecC, uint16_t>(a, s);
-    else region_launch<CodecC, uint32_t>(a, s);
+hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
+                         hipStream_t hs, hipEvent_t e0, hipEvent_t e1) {
+    if (wide) region_launch<CodecW, uint64_t>(a, s, hs, e0, e1);
+    else if (res_bytes == 1) region_launch<CodecC, uint8_t>(a, s, hs, e0, e1);
+    else if (res_bytes == 2) region_launch<CodecC, uint16_t>(a, s, hs, e0, e1);
+    else region_launch<CodecC, uint32_t>(a, s, hs, e0, e1);
     return hipGetLastError();
 }
 

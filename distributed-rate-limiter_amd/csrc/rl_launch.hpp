@@ -34,7 +34,13 @@ struct BatchCtl {
     unsigned long long cap_err;
     unsigned long long regions;
     unsigned long long cache_hits; // SW local-cache rejections (ratelimiter.cache.hits)
+    unsigned long long grow[4];    // limiter bit set: one of its regions is filling up
+    unsigned long long table_bytes;// state-table bytes read + written by the region stage
 };
+// A region holding more than kGrowUsed live keys after a batch (or one that overflowed)
+// flags its limiter for growth (rl_engine doubles its region count at the next status
+// collection): Redis grows its keyspace on demand (RedisRateLimitStorage.java:38-49).
+constexpr uint32_t kGrowUsed = 160;
 
 struct PartArgs {
     // pass 0 reads the caller's SoA request arrays
@@ -117,7 +123,7 @@ constexpr uint32_t kDbgWords = 8;        // debug words per bin
 // (block id mod kStatSlots), one 64-B line per slot; k_stats_reduce folds them into BatchCtl.
 constexpr uint32_t kStatSlots = 1024;
 enum : uint32_t { kStAllowed = 0, kStInvalid, kStCapErr, kStDistinct, kStRegions, kStCacheHits,
-                  kStCount, kStWords = 8 };
+                  kStTableBytes, kStCount, kStWords = 8 };
 
 struct HotInfo {             // one listed hot region
     uint64_t tag;            // its dominant key (mix64 of the key hash)
@@ -210,6 +216,8 @@ hipError_t launch_export(const Slot* table, uint64_t n_slots, const DevLimiter& 
                          int64_t now_ms, StateRec* out, uint32_t cap, uint32_t* count,
                          hipStream_t s);
 hipError_t launch_import(const ImportArgs& a, hipStream_t s);
+hipError_t launch_grow(const Slot* old_tab, const uint64_t* old_x, Slot* new_tab, uint64_t* new_x,
+                       uint64_t n_old_regions, int shard_bits, int k_new, int algo, hipStream_t s);
 hipError_t launch_sweep(Slot* table, uint64_t n_slots, const DevLimiter& L, int64_t now_ms,
                         uint32_t* count, hipStream_t s);
 
@@ -220,7 +228,10 @@ hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, ui
 hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hipStream_t s);
 hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
                            uint32_t cols, hipStream_t s);
-hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
+// hs (nullable): side stream for the hot chains (k_hot_chains), ordered by events e0 / e1;
+// without it the chains share the normal regions' launch (2-wave workgroups).
+hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
+                         hipStream_t hs = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s);
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s);   // prep, scan, summaries
 hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);

@@ -30,6 +30,8 @@ SW, TB = 0, 1
 OP_ACQUIRE, OP_PEEK, OP_RESET = 0, 1, 2
 REM_UNKNOWN, REM_INVALID, REM_ERROR = -1, -2, -3
 OPT_STAGE_TIMING = 1
+OPT_PIPELINE = 2       # RL_OPT_PIPELINE: partition of batch k+1 overlaps batch k's decisions
+OPT_FIXED_CAPACITY = 4  # RL_OPT_FIXED_CAPACITY: no on-demand table growth
 REGION_SLOTS = 256          # kRegionSlots in csrc/rl_device.hpp (state slots per region)
 MIN_REGIONS = 8             # kRegionsPerBin: every limiter has at least one bin of regions
 DIST_UNIFORM, DIST_ZIPF = 0, 1
@@ -46,6 +48,7 @@ EXPORTS = [
     "rl_route_unpack_return", "rl_route_partition_device", "rl_set_owner_directory",
     "rl_owner_of_engine", "rl_router_create", "rl_router_step", "rl_router_finish",
     "rl_router_plan_directory", "rl_router_destroy", "rl_pin_host", "rl_unpin_host",
+    "rl_grow_limiter", "rl_limiter_slots",
 ]
 RCCL_EXPORTS = ["rl_rccl_unique_id", "rl_transport_rccl_create", "rl_transport_rccl_destroy"]
 STATE_SW_BUCKET, STATE_TB_BUCKET = 0, 1
@@ -82,7 +85,7 @@ class LimiterConfig(ctypes.Structure):
 class BatchStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("n", "allowed", "distinct_keys", "invalid",
                                                  "capacity_errors", "regions_touched",
-                                                 "table_bytes", "cache_hits")]
+                                                 "table_bytes", "cache_hits", "table_grows")]
 
 
 class TraceSpec(ctypes.Structure):
@@ -163,6 +166,8 @@ def lib():
     L.rl_set_owner_directory.argtypes = [vp, sz, vp, vp]
     L.rl_owner_of_engine.argtypes = [vp, ctypes.c_uint64]
     L.rl_pin_host.argtypes = [vp, vp, sz]
+    L.rl_grow_limiter.argtypes = [vp, u16, ctypes.c_uint64]
+    L.rl_limiter_slots.argtypes = [vp, u16, ctypes.POINTER(ctypes.c_uint64)]
     L.rl_unpin_host.argtypes = [vp, vp]
     L.rl_owner_of_engine.restype = u32
     _lib = L
@@ -218,9 +223,10 @@ class Engine:
 
     def __init__(self, device: int = 0, max_batch: int = 1 << 22, capacity: int = 1 << 20,
                  stage_timing: bool = False, shard_index: int = 0, shard_count: int = 1,
-                 max_skew_ms: int = 0):
+                 max_skew_ms: int = 0, pipeline: bool = False, fixed_capacity: bool = False):
         self._L = lib()
-        o = Opts(device=device, flags=OPT_STAGE_TIMING if stage_timing else 0,
+        o = Opts(device=device, flags=(OPT_STAGE_TIMING if stage_timing else 0) |
+                 (OPT_PIPELINE if pipeline else 0) | (OPT_FIXED_CAPACITY if fixed_capacity else 0),
                  max_batch=max_batch, default_capacity=capacity, shard_index=shard_index,
                  shard_count=shard_count, max_skew_ms=max_skew_ms)
         h = ctypes.c_void_p()
@@ -282,6 +288,18 @@ class Engine:
         if st in (RL_E_DEVICE, RL_E_NOMEM, RL_E_TOO_LARGE):
             raise RlError(st, "rl_execute_batch")
         return allowed, remaining, tokens, st
+
+    def grow_limiter(self, limiter: int, min_keys: int) -> None:
+        st = self._L.rl_grow_limiter(self._h, limiter, min_keys)
+        if st != RL_OK:
+            raise RlError(st, "rl_grow_limiter")
+
+    def limiter_slots(self, limiter: int) -> int:
+        v = ctypes.c_uint64()
+        st = self._L.rl_limiter_slots(self._h, limiter, ctypes.byref(v))
+        if st != RL_OK:
+            raise RlError(st, "rl_limiter_slots")
+        return v.value
 
     def pin_host(self, arr) -> int:
         """rl_pin_host on a numpy array reused across host batches (status code)."""

@@ -100,6 +100,19 @@ typedef struct rl_opts {
 } rl_opts;
 
 #define RL_OPT_STAGE_TIMING 0x1u  /* record hipEvents around every stage (rl_stage_times) */
+/* Pipelined device batches: the partition of a batch (stages 1-3) runs on a second engine
+ * stream into one of two scratch sets, so it overlaps the previous batch's decision stage;
+ * decisions are still applied in submission order. It applies to rl_execute_batch_device
+ * calls with stream == NULL, whose inputs must then be complete when the call is made
+ * (results are complete when rl_sync / rl_last_status return). Calls with a stream and the
+ * host-buffer calls are ordered as without the option. Scratch memory doubles. */
+#define RL_OPT_PIPELINE     0x2u
+/* Fixed-size state tables. By default a limiter's table grows on demand, as the Redis
+ * keyspace does (RedisRateLimitStorage.java:38-49): when a batch leaves one of its regions
+ * more than 62.5 % full (or overflows one: those requests report RL_REMAINING_ERROR and the
+ * batch RL_E_CAPACITY), the region count doubles (twice after an overflow) when the batch's
+ * status is collected (rl_last_status, the host-buffer calls). */
+#define RL_OPT_FIXED_CAPACITY 0x4u
 
 #define RL_LIM_LOCAL_CACHE 0x1u  /* RateLimitConfig.enableLocalCache (RateLimitConfig.java:37-38) */
 
@@ -126,9 +139,12 @@ typedef struct rl_batch_stats {
     uint64_t invalid;           /* requests rejected as invalid                               */
     uint64_t capacity_errors;   /* requests not applied because a region was full            */
     uint64_t regions_touched;   /* state-table regions loaded + written back                  */
-    uint64_t table_bytes;       /* bytes of state-table regions moved (load + write-back)     */
+    uint64_t table_bytes;       /* state-table bytes read + written by the batch (whole 8 KB
+                                   region images both ways; sparse regions: the 128-B buckets
+                                   faulted in + the 32-B slots written back)                  */
     uint64_t cache_hits;        /* SW local-cache rejections (ratelimiter.cache.hits,
                                    SlidingWindowRateLimiter.java:75-77,96)                  */
+    uint64_t table_grows;       /* region-count doublings so far (on-demand table growth)   */
 } rl_batch_stats;
 
 /* Create / destroy an engine on one GPU. Replaces the JedisPool + Redis keyspace
@@ -142,6 +158,11 @@ void rl_destroy(rl_engine* e);
 int  rl_add_limiter(rl_engine* e, int algo, int64_t max_permits, int64_t window_ms,
                     double refill_per_s, uint16_t* id);
 int  rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* cfg, uint16_t* id);
+
+/* Grow a limiter's state table (doubling its regions, live state kept) until it holds
+ * min_keys keys at load <= 0.5; rl_limiter_slots reports its current slot count. */
+int  rl_grow_limiter(rl_engine* e, uint16_t limiter, uint64_t min_keys);
+int  rl_limiter_slots(rl_engine* e, uint16_t limiter, uint64_t* slots);
 
 /* tryAcquire over a batch of HOST buffers (pageable or pinned).
  *   allowed[i]      1 if request i acquired its permits

@@ -51,23 +51,31 @@ def synth(eng, cfg, t0_ns, n, index_base=0, steps=13):
     return keys, permits, now, lim
 
 
-def run_config(name, n, batches):
+def run_config(name, n, batches, pipeline=False, cuts=None):
+    """`pipeline`: RL_OPT_PIPELINE, every batch submitted back-to-back with no sync in between
+    (batch b+1's partition overlaps batch b's decisions); `cuts`: explicit batch boundaries."""
     cfgs, t0_ns = bench_configs()
     cfg = cfgs[name]
-    per = (n + batches - 1) // batches
-    eng = rl_amd.Engine(device=0, max_batch=per, capacity=cfg["capacity"])
+    if cuts is None:
+        per = (n + batches - 1) // batches
+        cuts = [min(n, b * per) for b in range(batches + 1)]
+    per = max(b - a for a, b in zip(cuts, cuts[1:]))
+    eng = rl_amd.Engine(device=0, max_batch=per, capacity=cfg["capacity"], pipeline=pipeline)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)
     keys, permits, now, lim = synth(eng, cfg, t0_ns, n)
     allowed = torch.empty(n, dtype=torch.uint8, device="cuda")
     remaining = torch.empty(n, dtype=torch.int64, device="cuda")
-    for b in range(batches):
-        sl = slice(b * per, min(n, (b + 1) * per))
+    torch.cuda.synchronize()                    # inputs complete before the (pipelined) calls
+    for a, b in zip(cuts, cuts[1:]):
+        sl = slice(a, b)
         m = sl.stop - sl.start
         eng.execute_device(m, keys[sl], permits[sl], now[sl], None if lim is None else lim[sl],
                            None, allowed[sl], remaining[sl])
-        assert eng.last_status() == rl_amd.RL_OK, rl_amd.strerror(eng.last_status())
+        if not pipeline:
+            assert eng.last_status() == rl_amd.RL_OK, rl_amd.strerror(eng.last_status())
     eng.sync()
+    assert eng.last_status() == rl_amd.RL_OK, rl_amd.strerror(eng.last_status())
     st = eng.stats()
     k = keys.cpu().numpy().view(np.uint64)
     p = permits.cpu().numpy()
@@ -87,6 +95,21 @@ def test_config_mixed_tenants_16m():
     k, got, st = run_config("mixed_tenants", 1 << 24, 2)
     _, c = np.unique(k, return_counts=True)
     assert c.max() > 16384                       # the hot path fired (hot_threshold)
+    assert 0 < got[0].sum() < len(k)
+
+
+def test_config_tb_uniform_pipelined():
+    """configs[1] (the default bench line) in 4 back-to-back batches with RL_OPT_PIPELINE."""
+    k, got, st = run_config("tb_uniform", 1 << 24, 4, pipeline=True)
+    assert 0 < got[0].sum() < len(k)
+
+
+def test_config_mixed_tenants_pipelined_ragged():
+    """Pipelined batches of ragged, growing sizes: each scratch set is regrown mid-stream
+    (two passes, hot path, 10 limiters), and a tiny batch sits between large ones."""
+    n = 3 << 22
+    cuts = [0, 1 << 20, (1 << 20) + 777, 3 << 21, (3 << 21) + (1 << 22) + 5, n]
+    k, got, _ = run_config("mixed_tenants", n, 0, pipeline=True, cuts=cuts)
     assert 0 < got[0].sum() < len(k)
 
 

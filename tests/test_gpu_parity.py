@@ -145,8 +145,8 @@ def test_ttl_reclamation_reuses_slots():
         k = np.repeat(k, 3)
         now = np.full(k.shape, (T0 + w * 10_000) * NS, np.int64) + np.arange(k.size) * 1000
         parts.append((k, np.ones(k.size, np.int32), now, (np.arange(k.size) % 2).astype(np.uint16)))
-    # capacity 1 -> each limiter has exactly one region
-    e = rl_amd.Engine(max_batch=1 << 16, capacity=1)
+    # capacity 1 -> each limiter has exactly one bin of regions; fixed, so slots are reused
+    e = rl_amd.Engine(max_batch=1 << 16, capacity=1, fixed_capacity=True)
     for l in lims:
         e.add_limiter(*l[:4], capacity=1)
     o = COracle([l[:4] for l in lims])
