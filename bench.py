@@ -200,8 +200,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--tune", action="append", default=[],
                     help="engine knob key=value (rl_tune), e.g. bin_shift=0")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="N=1: one stream, no overlap of consecutive batches")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="N=1: overlap batch s+1's partition with batch s's decisions (RL_OPT_PIPELINE)")
     ap.add_argument("--stage-timing", action="store_true",
                     help="also record hipEvents inside the timed steps (diagnostics only)")
     args = ap.parse_args()
@@ -231,11 +231,11 @@ def main():
     # is sized for its share of the global key population.
     # an owner can receive up to ws x n requests in a skewed step (the router grows its
     # receive buffers; the engine's scratch is allocated for what it actually receives)
-    # N=1: pipelined device batches (RL_OPT_PIPELINE): batch s+1's partition runs on a second
-    # stream while batch s's decisions are applied (inputs are HBM-resident and complete)
+    # --pipeline (N=1): RL_OPT_PIPELINE, batch s+1's partition on a second stream while batch s's
+    # decisions are applied; measured slower on tb_uniform, so off by default
     eng = rl_amd.Engine(device=local, max_batch=n * ws,
                         capacity=cfg["capacity"] * ws, stage_timing=False, shard_index=rank,
-                        shard_count=ws, pipeline=ws == 1 and not args.no_pipeline)
+                        shard_count=ws, pipeline=ws == 1 and args.pipeline)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)
     for kv in args.tune:

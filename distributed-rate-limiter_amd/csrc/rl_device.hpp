@@ -241,6 +241,7 @@ __host__ __device__ inline int res_bytes_for(int64_t max_permits, bool wide) {
 
 // Java (long) narrowing of a double (JLS 5.1.3) / Redis (long long) of a Lua number.
 __device__ inline int64_t d2l(double d) {
+    if (__builtin_expect(__builtin_fabs(d) < 2147483648.0, 1)) return (int64_t)(int32_t)d;  // one cvt
     if (d != d) return 0;
     if (d >= 9223372036854775807.0) return INT64_MAX;
     if (d <= -9223372036854775808.0) return INT64_MIN;
@@ -267,12 +268,14 @@ __device__ inline double tb_refill(const DevLimiter& L, int64_t now, uint64_t a,
     const int64_t last = (int64_t)b;
     const bool exists = (c & 1u) && !(now > last + L.ttl_ms);
     const double capacity = L.capacity;
-    const double nowd = (double)now;
-    const double tokens = exists ? __longlong_as_double((long long)a) : capacity;
-    const double last_refill = exists ? (double)last : nowd;
-    const double elapsed = nowd - last_refill;               // Lua :56
+    // absent or expired: tokens = capacity, last_refill = now, so elapsed = 0 and the balance
+    // is min(capacity, capacity + 0 * rate) = capacity exactly
+    if (!exists) return capacity;
+    // Lua :56: now - last_refill on doubles is exact (both are integers below 2^53 and so is
+    // their difference), i.e. the same as converting the integer difference once
+    const double elapsed = (double)(now - last);
     const double tokens_to_add = elapsed * L.rate_per_ms;    // Lua :57
-    const double x = tokens + tokens_to_add;                 // Lua :58
+    const double x = __longlong_as_double((long long)a) + tokens_to_add;   // Lua :58
     return x < capacity ? x : capacity;                      // math.min(capacity, x)
 }
 

@@ -55,6 +55,11 @@ __device__ inline uint64_t wave_match(uint32_t v, int nbits, bool active) {
     return m;
 }
 
+__device__ inline uint64_t readlane64(uint64_t v, uint32_t lane) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)lane) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)lane);
+}
+
 __device__ inline uint64_t ord_key(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ULL; }
 
 // Earliest / latest now_ms of the batch's valid requests. A batch with no valid request
@@ -466,6 +471,11 @@ struct RegionTable {
     uint64_t sb[kRegionSlots];
     uint64_t sc[kRegionSlots];
     alignas(16) uint32_t occ[kRegionSlots];   // bit0 occupied, bit1 touched by this batch
+#ifdef RL_CHAINS
+    int64_t xrem[64];                         // wave_apply's per-key chains: results by lane
+    double xtok[64];
+    uint32_t xalw[64];
+#endif
 };
 // With a sliding-window local cache (SlidingWindowRateLimiter.java:57-64): every slot also
 // carries its key's cache state (block-until ms, sw_step_cache), moved with the slot.
@@ -548,6 +558,58 @@ __device__ inline void note_fill(const RegionArgs& a, uint32_t region, uint32_t 
         atomicOr(&a.ctl->grow[li >> 6], 1ULL << (li & 63));
     }
 }
+
+#ifdef RL_CHAINS
+// A/B build only (-DRL_CHAINS): measured slower than the rounds on every bench config
+// (same-box A/B: tb_uniform region 1.21 -> 1.28 ms, zipf_1b 6.16 -> 6.64, mixed 13.93 -> 14.03).
+// The per-key chains of wave_apply: every pending lane's key has its state in S[slot]; the
+// lowest pending lane of each key runs that key's pending requests in lane (= arrival) order,
+// reading each request's fields from its lane; results go through LDS back to their lanes.
+template <class Codec, int ALGO, class LdsT>
+__device__ inline void wave_chains(LdsT& S, const DevLimiter& L, uint32_t lane, const Req& q,
+                                   const SWGeo& geo, int32_t slot, bool& pending, uint64_t kp,
+                                   Applied& r, uint32_t& n_allowed) {
+    const bool leader = pending && (kp & ((1ULL << lane) - 1)) == 0;
+    uint64_t todo = leader ? kp : 0ULL;
+    uint64_t sa = 0, sb = 0, sc = 0;
+    if (leader) { sa = S.sa[slot]; sb = S.sb[slot]; sc = S.sc[slot]; }
+    while (__any(todo != 0)) {
+        const bool act = todo != 0;
+        const uint32_t l = act ? (uint32_t)__builtin_ctzll(todo) : lane;
+        todo &= todo - 1;
+        // every lane takes part in the shuffles (a source lane may be idle)
+        const int64_t t_l = __shfl(q.now_ms, (int)l, 64);
+        const int32_t p_l = __shfl(q.permits, (int)l, 64);
+        const uint32_t op_l = (uint32_t)__shfl((int)q.op, (int)l, 64);
+        Outcome o{};
+        if constexpr (ALGO == kAlgoTB) {
+            if (act) o = tb_step(L, op_l, p_l, t_l, sa, sb, sc);
+        } else {
+            SWGeo g;
+            g.curr_start = __shfl(geo.curr_start, (int)l, 64);
+            g.prev_start = __shfl(geo.prev_start, (int)l, 64);
+            g.prev_weight = __shfl(geo.prev_weight, (int)l, 64);
+            if (act) o = sw_step_g(L, op_l, p_l, t_l, g, sa, sb, sc);
+        }
+        if (act) {
+            S.xrem[l] = o.remaining;
+            S.xtok[l] = o.tokens;
+            S.xalw[l] = o.allowed ? 1u : 0u;
+            if (o.mutate) { sa = o.a; sb = o.b; sc = o.c; }
+        }
+    }
+    if (leader) { S.sa[slot] = sa; S.sb[slot] = sb; S.sc[slot] = sc; }
+    wave_fence();
+    if (pending) {
+        r.alw = S.xalw[lane] != 0;
+        r.rem = S.xrem[lane];
+        r.tok = S.xtok[lane];
+        n_allowed += r.alw ? 1u : 0u;
+        pending = false;
+    }
+    wave_fence();
+}
+#endif
 
 // Apply one group of up to 64 requests (lane order = arrival order; `valid` lanes only).
 // SP: the region may be sparse (unloaded buckets, tombstones); image regions (SP = false)
@@ -668,7 +730,26 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         same_w = ((wi & 1) ? b0 : ~b0) & ((wi & 2) ? b1 : ~b1);
         elig_m = __ballot(slot >= 0 && wi < 3 && q.op == (uint32_t)kOpAcquire);
     }
+    uint32_t my_rounds = 0;
     while (__any(pending)) {
+        // Chains: after two rounds, if every key still pending has changed state in (nearly)
+        // every round so far (runs of TB allows, SW allows across windows) and some key still
+        // has >= 4 requests pending, the rounds would go on finalizing one request per key
+        // each; the lowest pending lane of every key then applies the key's remaining
+        // requests itself, in arrival order (each a full exact step; a deny leaves the state
+        // as it is), instead of one wave round per state change.
+#ifdef RL_CHAINS
+        if (!CACHE && my_rounds >= 2 && !one_round) {
+            const uint64_t kp = peers & __ballot(pending);
+            const uint32_t fin = (uint32_t)__popcll(peers) - (uint32_t)__popcll(kp);
+            if (__all(!pending || fin <= 2u * my_rounds) && __any(pending && __popcll(kp) >= 4)) {
+                ++n_rounds;
+                wave_chains<Codec, ALGO>(S, L, lane, q, geo, slot, pending, kp, r, n_allowed);
+                break;
+            }
+        }
+#endif
+        ++my_rounds;
         ++n_rounds;
         Outcome o{};
         SWAllow al{false, 0};
@@ -690,10 +771,15 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                         o = sw_step_cache(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc, S.sx[slot], hit);
                 } else {
                     o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc);
-                    // (A) needs: all pending peers acquires in one window, not before the
-                    // newest bucket, and more than one of them
-                    elig = (kp & ~(elig_m & same_w)) == 0 && (kp & (kp - 1)) != 0 &&
-                           (int64_t)sa <= geo.curr_start;
+                    // (A) for this request needs: it and every EARLIER pending peer are
+                    // acquires in its window, not before the key's newest bucket (the allows
+                    // of one window then only INCR its bucket). A later window's requests
+                    // become eligible in the next round, once this window's are final.
+                    const uint64_t upto = kp & (((1ULL << lane) - 1) | (1ULL << lane));
+                    // (near the epoch, now < w, Java's truncating division makes the previous
+                    // window the current one, :170-172: its count then moves with the allows)
+                    elig = (upto & ~(elig_m & same_w)) == 0 && (int64_t)sa <= geo.curr_start &&
+                           geo.prev_start != geo.curr_start;
                     if (elig) al = sw_try_after_allows(L, q.permits, q.now_ms, geo, sa, sb, sc,
                                                        popc_below(kp));
                 }
@@ -702,15 +788,22 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         const uint64_t mut = __ballot(pending && o.mutate) & peers;
         const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
         bool use_a = false;
-        uint32_t fa = 64u;
+        uint32_t fa = 64u, a_end = 0u;
         if constexpr (!tb) {
+            // per key: (A) is final up to its first denial (inclusive) or its first pending
+            // request that is not eligible (exclusive); (D) up to the first state change
             const uint64_t den = __ballot(pending && elig && !al.allowed) & peers;
-            fa = den ? (uint32_t)__builtin_ctzll(den) : 64u;
-            use_a = elig && fa > fm;             // the allow hypothesis decides more
+            const uint64_t nel = __ballot(pending && !elig) & peers;
+            const uint32_t fd = den ? (uint32_t)__builtin_ctzll(den) : 64u;
+            const uint32_t fs = nel ? (uint32_t)__builtin_ctzll(nel) : 64u;
+            fa = fd < fs ? fd : fs;                 // allows: the pending peers below fa
+            a_end = fd < fs ? fd + 1u : fs;
+            const uint32_t d_end = fm < 64u ? fm + 1u : 64u;
+            use_a = a_end > d_end;               // the allow hypothesis decides more
         }
         if (pending && use_a) {
             if constexpr (!tb) {
-                if (lane <= fa) {
+                if (lane < a_end) {
                     const uint64_t ok = kp & (fa >= 64u ? ~0ULL : ((1ULL << fa) - 1));   // the allows
                     if (ok && lane == 63u - (uint32_t)__builtin_clzll(ok)) {   // the last allow commits
                         uint64_t na = S.sa[slot], nb = S.sb[slot], nc = S.sc[slot];
@@ -1423,10 +1516,10 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         n_allowed += o.allowed ? 1u : 0u;
                         pend = false;
                     }
-                    if (fm < 64u) {
-                        sa = __shfl(o.a, (int)fm, 64);
-                        sb = __shfl(o.b, (int)fm, 64);
-                        sc = __shfl(o.c, (int)fm, 64);
+                    if (fm < 64u) {                        // fm is wave-uniform: read lanes
+                        sa = readlane64(o.a, fm);
+                        sb = readlane64(o.b, fm);
+                        sc = readlane64(o.c, fm);
                         changed = true;
                     }
                 }
@@ -1443,9 +1536,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 const int64_t w = L.window_ms, mx = L.max_permits;
                 while (__any(pend)) {
                     const uint32_t f0 = (uint32_t)__builtin_ctzll(__ballot(pend));
-                    const int64_t W0 = __shfl(geo.curr_start, (int)f0, 64);
+                    const int64_t W0 = (int64_t)readlane64((uint64_t)geo.curr_start, f0);
                     const bool scan = pend && q.op == (uint32_t)kOpAcquire && geo.curr_start == W0 &&
-                                      (int64_t)sa <= W0;
+                                      (int64_t)sa <= W0 && geo.prev_start != geo.curr_start;
                     const uint64_t und = __ballot(pend && !scan);
                     const uint32_t stop = und ? (uint32_t)__builtin_ctzll(und) : 64u;
                     const bool in = scan && lane < stop;
@@ -1495,7 +1588,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         // the exact step of request `stop` alone (wave-uniform arithmetic)
                         const uint32_t op_s = (uint32_t)__builtin_amdgcn_readlane((int)q.op, (int)stop);
                         const int32_t p_s = __builtin_amdgcn_readlane(q.permits, (int)stop);
-                        const int64_t t_s = __shfl(q.now_ms, (int)stop, 64);
+                        const int64_t t_s = (int64_t)readlane64((uint64_t)q.now_ms, stop);
                         const Outcome o = sw_step_g(L, op_s, p_s, t_s, sw_geo(t_s, L), sa, sb, sc);
                         if (lane == stop) {
                             oa = o.allowed;
@@ -1733,7 +1826,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 #define RL_REGION_MIN_WAVES 4
 #endif
 template <class Codec, class Res, bool TOK, int BS, bool HOT, bool CACHE = false>
-__global__ __launch_bounds__(HOT ? 128 : 64, HOT ? RL_HOT_MIN_WAVES : RL_REGION_MIN_WAVES) void k_regions(RegionArgs a) {
+__global__ __launch_bounds__(HOT ? 128 : 64, HOT ? RL_HOT_MIN_WAVES : BS > 0 ? 3 : RL_REGION_MIN_WAVES)
+void k_regions(RegionArgs a) {
     if constexpr (CACHE) {                       // some limiter keeps a local cache (BS 0, no hot path)
         __shared__ RegionTableX S;
         region_body_t<Codec, Res, TOK, 0>(a, blockIdx.x, S);

@@ -385,3 +385,24 @@ def test_pinned_host_buffers_match_pageable():
         assert e.unpin_host(b) == rl_amd.RL_OK
     assert e.unpin_host(bufs["keys"]) == rl_amd.RL_E_INVALID_ARG   # no longer pinned
     o.close()
+
+
+@pytest.mark.parametrize("algo", [rl_amd.SW, rl_amd.TB])
+def test_medium_hot_keys_across_windows(algo):
+    """Keys just below the hot-path threshold with 1-s windows: a 64-request group spans
+    window boundaries (per-window allow prefixes) and long allow chains (per-key chains)."""
+    rng = np.random.default_rng(77 + algo)
+    lims = [[algo, 100, 1_000, 60.0 if algo == rl_amd.TB else 0.0],
+            [algo, 5, 1_000, 2.0 if algo == rl_amd.TB else 0.0]]
+    n = 400_000
+    hot = rl_amd.mix64(np.arange(12, dtype=np.uint64) + np.uint64(99 << 40))
+    cold = rl_amd.mix64(rng.integers(0, 50_000, n).astype(np.uint64))
+    keys = np.where(rng.random(n) < 0.9, hot[rng.integers(0, 12, n)], cold)
+    lim = (rl_amd.mix64(keys) & np.uint64(1)).astype(np.uint16)
+    now = (T0 * NS + np.sort(rng.integers(0, 20_000 * NS, n))).astype(np.int64)
+    permits = rng.integers(1, 3, n).astype(np.int32)
+    op = np.zeros(n, np.uint8)
+    op[rng.random(n) < 0.002] = 1
+    got, want, _ = run_both(lims, (keys, permits, now, lim, op), batches=3,
+                            capacity=1 << 16)
+    assert_same(got, want, "medium-hot")
