@@ -42,12 +42,15 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 // Partition tiles (upsweep / scatter / unpermute all share this tiling). 64K
 // requests per tile; grids are persistent (one workgroup per CU) and walk the tiles
 // so that the 32 workgroups of an XCD work on 32 consecutive tiles at a time.
+// 8 waves per tile (2 per SIMD): the scatter is latency-bound at one wave per SIMD, and
+// more workgroups per CU would put more tiles' partial record lines in flight per L2
+// (same-box A/B, tb_uniform: 3.60 -> 3.24 ms/step vs 4 waves per tile).
 #ifndef RL_TILE_THREADS
-#define RL_TILE_THREADS 256
+#define RL_TILE_THREADS 512
 #endif
 constexpr int kTileThreads = RL_TILE_THREADS;
 #ifndef RL_TILE_ITEMS
-#define RL_TILE_ITEMS 256                          // per-thread items per tile (A/B builds: -DRL_TILE_ITEMS)
+#define RL_TILE_ITEMS 128                          // per-thread items per tile (A/B builds: -DRL_TILE_ITEMS)
 #endif
 constexpr int kTileItems = RL_TILE_ITEMS;
 constexpr int kTile = kTileThreads * kTileItems;  // 65536 requests per tile (default)

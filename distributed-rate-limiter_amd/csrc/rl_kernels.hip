@@ -47,10 +47,13 @@ __device__ inline uint32_t popc_below(uint64_t m) {
 // Lanes of this wave whose `v` (low nbits) equals mine, among `active` lanes.
 __device__ inline uint64_t wave_match(uint32_t v, int nbits, bool active) {
     uint64_t m = __ballot(active);
-    for (int b = 0; b < nbits; ++b) {
-        const bool bit = (v >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        m &= bit ? bb : ~bb;
+#pragma unroll
+    for (int b = 0; b < kMaxDigitBits; ++b) {
+        if (b < nbits) {                             // wave-uniform
+            const bool bit = (v >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
     }
     return m;
 }
@@ -330,8 +333,11 @@ constexpr int kScatterDepth = RL_SCATTER_DEPTH;   // rounds of inputs in flight 
 template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     using Rec = typename Codec::Rec;
+    static_assert(kTileThreads / 64 <= 8, "per-wave counts are packed 8 to a bin");
     __shared__ uint32_t cur[1u << kMaxDigitBits];                    // next slot per bin
-    __shared__ uint8_t cntw[kTileThreads / 64][1u << kMaxDigitBits]; // this round, per wave
+    // this round's count of each wave per bin, the waves' bytes packed in one word: a lane
+    // sums the earlier waves' counts for its bin with one read and two v_sad_u8
+    __shared__ uint64_t cntw[1u << kMaxDigitBits];
     __shared__ LimLds L;
     __shared__ uint64_t s_mm[2][kTileThreads / 64];
     const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -349,8 +355,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
         __syncthreads();     // previous tile's LDS users are done
         for (uint32_t b = t; b < bins; b += kTileThreads) {
             cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
-#pragma unroll
-            for (int w = 0; w < kTileThreads / 64; ++w) cntw[w][b] = 0;
+            cntw[b] = 0;
         }
         // kScatterDepth rounds of inputs in flight; out-of-range lanes re-load element n-1
         // so every wave issues the same loads and stores each round (static vmcnt counting)
@@ -399,17 +404,18 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
             const uint32_t lr = popc_below(m);
             const uint32_t cnt = (uint32_t)__popcll(m);
             const bool leader = active && lr == 0;
-            if (leader) cntw[wid][d] = (uint8_t)cnt;
+            if (leader) ((uint8_t*)&cntw[d])[wid] = (uint8_t)cnt;
             if (!(abl & kAblNoBarrier)) __syncthreads();
             uint32_t pos = 0;
             if (active) {
-                pos = cur[d] + lr;
-                for (uint32_t w = 0; w < wid; ++w) pos += cntw[w][d];
+                const uint64_t below = wid == 0 ? 0ULL : cntw[d] & ((1ULL << (8 * wid)) - 1);
+                pos = cur[d] + lr + __builtin_amdgcn_sad_u8((uint32_t)below, 0u, 0u) +
+                      __builtin_amdgcn_sad_u8((uint32_t)(below >> 32), 0u, 0u);
             }
             if (!(abl & kAblNoBarrier)) __syncthreads();
             if (leader) {
                 atomicAdd(&cur[d], cnt);
-                cntw[wid][d] = 0;
+                ((uint8_t*)&cntw[d])[wid] = 0;
             }
             if (abl & (kAblNoMatch | kAblNoBarrier)) pos = min(pos, a.n - 1);
             // inactive lanes write to the padding slot past n (buffers carry spare entries)
@@ -730,7 +736,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         same_w = ((wi & 1) ? b0 : ~b0) & ((wi & 2) ? b1 : ~b1);
         elig_m = __ballot(slot >= 0 && wi < 3 && q.op == (uint32_t)kOpAcquire);
     }
-    uint32_t my_rounds = 0;
+    [[maybe_unused]] uint32_t my_rounds = 0;      // -DRL_CHAINS only
     while (__any(pending)) {
         // Chains: after two rounds, if every key still pending has changed state in (nearly)
         // every round so far (runs of TB allows, SW allows across windows) and some key still
