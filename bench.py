@@ -200,6 +200,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--tune", action="append", default=[],
                     help="engine knob key=value (rl_tune), e.g. bin_shift=0")
+    ap.add_argument("--table-scale", type=int, default=1,
+                    help="size the state tables for this many times the config's key count "
+                         "(engine sizing: lower load, more and smaller regions)")
     ap.add_argument("--pipeline", action="store_true",
                     help="N=1: overlap batch s+1's partition with batch s's decisions (RL_OPT_PIPELINE)")
     ap.add_argument("--stage-timing", action="store_true",
@@ -234,7 +237,8 @@ def main():
     # --pipeline (N=1): RL_OPT_PIPELINE, batch s+1's partition on a second stream while batch s's
     # decisions are applied; measured slower on tb_uniform, so off by default
     eng = rl_amd.Engine(device=local, max_batch=n * ws,
-                        capacity=cfg["capacity"] * ws, stage_timing=False, shard_index=rank,
+                        capacity=cfg["capacity"] * ws * args.table_scale, stage_timing=False,
+                        shard_index=rank,
                         shard_count=ws, pipeline=ws == 1 and args.pipeline)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)

@@ -40,7 +40,10 @@ struct BatchCtl {
 // A region holding more than kGrowUsed live keys after a batch (or one that overflowed)
 // flags its limiter for growth (rl_engine doubles its region count at the next status
 // collection): Redis grows its keyspace on demand (RedisRateLimitStorage.java:38-49).
-constexpr uint32_t kGrowUsed = 160;
+// 208 of 256: at the design load (0.5, 128 keys per region on average) the fullest of 8192
+// regions holds ~128 + 4.5 sigma ~ 180 keys, so a table at its configured capacity does not
+// grow; at ~0.62 average load it does, well before the fullest region (~217) overflows.
+constexpr uint32_t kGrowUsed = 208;
 
 struct PartArgs {
     // pass 0 reads the caller's SoA request arrays
