@@ -1504,6 +1504,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 }
             }
             bool changed = false;
+            bool t_fresh = false;                         // [T0, T1) is for the current state
             const uint64_t c_run = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
             if constexpr (A == kAlgoTB) {
                 // token bucket: rounds; each applies the prefix up to the first state change
@@ -1527,6 +1528,25 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         sb = readlane64(o.b, fm);
                         sc = readlane64(o.c, fm);
                         changed = true;
+                        t_fresh = false;
+                        // the later requests inside the new state's [T0, T1) are denied
+                        // with remaining 0 by time alone (a key at its limit: the balance
+                        // stays below 1 for a while after an allow), not by another round
+                        if (__any(pend)) {
+                            T0 = hot_t0<A>(lo, hi, sa, sb, sc);
+                            T1 = hot_t1_lb<A>(L, sa, sb, sc, T0, hi);
+                            t_fresh = true;
+                            ++n_tk;
+                            const bool fast = q.op == (uint32_t)kOpAcquire && q.now_ms >= T0 && q.now_ms < T1;
+                            const uint64_t m = __ballot(pend && !fast);
+                            const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+                            if (pend && lane < first) {
+                                oa = false;
+                                orem = 0;
+                                if (TOK) tk = tb_refill(L, q.now_ms, sa, sb, sc);
+                                pend = false;
+                            }
+                        }
                     }
                 }
             } else {
@@ -1619,7 +1639,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             // (no chunk could be skipped anyway: recomputed after a chunk without a change)
             const uint64_t c_srch = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
             const bool dense = c == prev_detail + 1;
-            if (changed && dense) {
+            if (t_fresh) {
+                stale = false;                            // computed after the last change
+            } else if (changed && dense) {
                 T0 = hot_t0<A>(lo, hi, sa, sb, sc);
                 T1 = T0;
                 stale = true;
