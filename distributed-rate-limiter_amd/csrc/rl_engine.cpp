@@ -98,6 +98,8 @@ struct rl_engine {
     hipStream_t hstream = nullptr;          // hot chains beside the normal regions
     hipEvent_t hot_ev[2] = {};              // fork / join of hstream
     bool split_hot = true;                  // rl_tune("split_hot"): 0 = one 2-wave launch
+    uint32_t region_walk = 0;               // rl_tune("region_walk"): persistent waves per CU
+    uint32_t* d_work = nullptr;             // its claim counters (8 x 64 B)
     // hot regions
     uint32_t* hot_list = nullptr;           // [kHotMax + 40]: list, k_hot_select's meta, total
     HotInfo* hot_info = nullptr;            // [kHotMax]
@@ -263,6 +265,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
              hipEventCreateWithFlags(&B.freed, hipEventDisableTiming) != hipSuccess))
             rc = RL_E_DEVICE;
     }
+    if (rc == RL_OK) rc = dalloc(&e->d_work, 128);
     if (rc == RL_OK) rc = dalloc(&e->d_stats, (size_t)kStatSlots * kStWords);
     if (rc == RL_OK && hipMemset(e->d_stats, 0, (size_t)kStatSlots * kStWords * 8) != hipSuccess)
         rc = RL_E_DEVICE;
@@ -293,7 +296,7 @@ extern "C" void rl_destroy(rl_engine* e) {
         if (B.freed) (void)hipEventDestroy(B.freed);
     }
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
-    dfree(e->d_stats);
+    dfree(e->d_stats); dfree(e->d_work);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
     dfree(e->route_scratch); dfree(e->route_counts); dfree(e->d_dir);
@@ -666,6 +669,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
     ra.skew_ms = e->opts.max_skew_ms;
     ra.stats = e->d_stats;
+    ra.work = e->d_work;
+    ra.walk = e->region_walk;
     ra.cache = cache ? 1u : 0u;
     ra.sparse_max = bsh == 0 ? e->sparse_max : 0u;
     if (e->debug_regions) {
@@ -969,6 +974,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "sparse_max") == 0) {         // records per region; 0 = image mode only
         if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
         e->sparse_max = (uint32_t)value;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "region_walk") == 0) {       // 0 = one workgroup per region
+        if (value < 0 || value > 32) return RL_E_INVALID_ARG;
+        e->region_walk = (uint32_t)value;
         return RL_OK;
     }
     if (std::strcmp(key, "split_hot") == 0) {

@@ -107,6 +107,9 @@ struct RegionArgs {
     uint64_t* hot_summ;        // [chunks][4]: k_hot_summ's summary, then the chain's verdict
     uint64_t* hot_summ2;       // [groups][4]: the same over 64 chunks (4096 records)
     uint32_t* hot_total;       // [0] chunks, [1] groups over the listed regions
+    uint32_t* work;            // region walk (walk > 0): 8 claim counters, 64 B apart, zeroed
+    uint32_t walk;             // rl_tune("region_walk"): persistent normal-region waves per CU
+                               // claiming regions from `work` (0: one workgroup per region)
     uint64_t* dbg;             // nullable (rl_tune "debug_regions"): per bin kDbgWords words
                                // {t_start, t_end, records, rounds, 4 x cycle counters}
 };

@@ -136,3 +136,94 @@ def test_wire_pack_unwire_roundtrip():
     eng.route_pack_wire(n, td(perm), td(keys), td(permits), td(now2), None, wire, None, hdr)
     eng.sync()
     assert hdr.cpu().tolist()[1] == 1
+
+
+def _bench_worker(rank, world, port, cfg_name, steps, n, out):
+    """One rank of bench.py's N-GPU path on the shared GPU: its slice of the exact bench
+    trace (k_synth, same seed / key population / time axis as `bench.py --gpus world`)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import rl_amd
+    from rl_amd.router import DeviceOps, Router
+    cfg = bench.CONFIGS[cfg_name]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    eng = rl_amd.Engine(device=0, max_batch=world * n, capacity=1 << 22, shard_index=rank,
+                        shard_count=world)
+    for l in cfg["limiters"]:
+        eng.add_limiter(*l)
+    router = Router(DeviceOps(eng, world, dev, n), world, rank, exchange_device="cpu")
+    res_a, res_r = [], []
+    for s in range(steps):
+        k, p, t, li = _bench_slice(eng, cfg, s, rank, world, steps, n)
+        eng.sync()                                  # k_synth ran on the engine stream
+        a = torch.empty(n, dtype=torch.uint8, device=dev)
+        r = torch.empty(n, dtype=torch.int64, device=dev)
+        router.step(k, p, t, a, r, li)
+        eng.sync()
+        res_a.append(a.cpu().numpy())
+        res_r.append(r.cpu().numpy())
+    assert router.finish() == rl_amd.RL_OK
+    np.savez(f"{out}.{rank}.npz", a=np.concatenate(res_a), r=np.concatenate(res_r))
+    dist.destroy_process_group()
+
+
+def _bench_slice(eng, cfg, s, rank, world, steps, n):
+    import bench
+    dev = torch.device("cuda", 0)
+    n_lim = len(cfg["limiters"])
+    k = torch.empty(n, dtype=torch.int64, device=dev)
+    p = torch.empty(n, dtype=torch.int32, device=dev)
+    t = torch.empty(n, dtype=torch.int64, device=dev)
+    li = torch.empty(n, dtype=torch.int16, device=dev) if n_lim > 1 else None
+    eng.synth_trace(n, k, p, t, li, seed=cfg["seed"], n_keys=cfg["n_keys"] * world,
+                    dist=cfg["dist"], zipf_s=cfg.get("zipf_s", 1.1), permits_max=cfg["permits_max"],
+                    t0_ns=bench.T0_NS, span_ns=cfg["span_ns"] * steps,
+                    index_base=(s * world + rank) * n, n_total=steps * world * n, n_limiters=n_lim)
+    return k, p, t, li
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cfg_name", ["mixed_tenants", "zipf_1b"])
+def test_two_shards_bench_configs(tmp_path, cfg_name):
+    """BASELINE configs[3] / [4] (bench.py's 10-limiter and TB + SW Zipf workloads) through
+    the 2-shard router, 2M requests per rank per step, against the oracle on the global stream."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import rl_amd
+    from oracle.coracle import COracle
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world, steps, n = 2, 2, 1 << 21
+    out = str(tmp_path / "b")
+    mp.spawn(_bench_worker, args=(world, port, cfg_name, steps, n, out), nprocs=world, join=True)
+    cfg = bench.CONFIGS[cfg_name]
+    torch.cuda.set_device(0)
+    gen = rl_amd.Engine(device=0, max_batch=n, capacity=1 << 10)
+    parts = [[], [], [], []]
+    for st in range(steps):
+        for rank in range(world):
+            xs = _bench_slice(gen, cfg, st, rank, world, steps, n)
+            gen.sync()
+            for i, x in enumerate(xs):
+                parts[i].append(x.cpu().numpy())
+    gen.close()
+    keys = np.concatenate(parts[0]).view(np.uint64)
+    permits, now = np.concatenate(parts[1]), np.concatenate(parts[2])
+    lim = np.concatenate(parts[3]).view(np.uint16)
+    o = COracle(cfg["limiters"], nthreads=16)
+    wa, wr, _, _ = o.run(keys, permits, now, lim, want_tokens=False)
+    o.close()
+    assert 0 < wa.sum() < wa.size
+    for rank in range(world):
+        d = np.load(f"{out}.{rank}.npz")
+        for st in range(steps):
+            sl = slice((st * world + rank) * n, (st * world + rank + 1) * n)
+            assert np.array_equal(d["a"][st * n:(st + 1) * n], wa[sl]), (rank, st)
+            assert np.array_equal(d["r"][st * n:(st + 1) * n], wr[sl]), (rank, st)
