@@ -320,6 +320,10 @@ def main():
     value = ws * n * steps / elapsed
 
     kern = {k: v for k, v in stages.items() if k not in ("total", "region_offsets") and v > 0}
+    if kern.get("scatter1", 0.0) < 0.05 * kern.get("scatter0", 1.0):
+        # one partition pass: the pass-1 marks only bracket empty time
+        for k in ("upsweep1", "scan1", "scatter1"):
+            kern.pop(k, None)
     U = stats["distinct_keys"]
     n_lim = len(cfg["limiters"])
     req_bytes = REQ_IN + (2 if n_lim > 1 else 0) + REQ_OUT
