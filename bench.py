@@ -153,8 +153,10 @@ def config1_line(dev):
             "engine_value": n / best, "engine_ms": best * 1e3,
             "cpu_port_value": n / cpu_s, "cpu_port_cores": 1,
             "reference_published": 80192, "unit": "decisions/s",
-            "note": "engine = one HBM-resident batch (hot-key chain of 100k requests); the "
-                    "micro-batched host path is timed by tests/cpp/test_host_api (config1)"}
+            "note": "engine = one HBM-resident batch: the 100k requests share one key, so one "
+                    "region wave applies them 64 at a time (each group's allow run in one round, "
+                    "local cache on); the micro-batched host path is timed by "
+                    "tests/cpp/test_host_api (config1)"}
 
 
 def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remaining):

@@ -759,7 +759,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         ++n_rounds;
         Outcome o{};
         SWAllow al{false, 0};
-        bool elig = false, hit = false;
+        bool elig = false, hit = false, xs = false;
         const uint64_t pm = __ballot(pending);
         const uint64_t kp = peers & pm;                        // my key's pending requests
         if (pending) {
@@ -771,10 +771,26 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 if constexpr (tb) {
                     o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
                 } else if (cache_on) {
-                    // local cache on: every put may change the cache state, so one state
-                    // change per key per round (hypothesis D only)
-                    if constexpr (CACHE)
-                        o = sw_step_cache(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc, S.sx[slot], hit);
+                    if constexpr (CACHE) {
+                        const uint64_t x0 = S.sx[slot];
+                        o = sw_step_cache(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc, x0, hit);
+                        // (A) with the local cache: while the key has no cache entry that
+                        // rejects (x0 == 0) a put changes nothing unless its value reaches
+                        // max (:106-108, :119-121), so a run of allows is still closed-form;
+                        // the request whose put sets the entry (xs) ends the run, inclusive
+                        const uint64_t upto = kp & (((1ULL << lane) - 1) | (1ULL << lane));
+                        elig = x0 == 0 && (upto & ~(elig_m & same_w)) == 0 &&
+                               (int64_t)sa <= geo.curr_start && geo.prev_start != geo.curr_start;
+                        if (elig) {
+                            const uint32_t k = popc_below(kp);
+                            al = sw_try_after_allows(L, q.permits, q.now_ms, geo, sa, sb, sc, k);
+                            const SW2 s0 = sw_unpack(sa, sb, sc);
+                            const int64_t curr0 = s0.b1_start == geo.curr_start ? (int64_t)s0.b1_cnt : 0;
+                            // allow: newCount = curr0 + k + 1; deny: the estimate, >= max iff
+                            // its remaining is 0
+                            xs = al.allowed ? curr0 + (int64_t)k + 1 >= L.max_permits : al.remaining == 0;
+                        }
+                    }
                 } else {
                     o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc);
                     // (A) for this request needs: it and every EARLIER pending peer are
@@ -798,12 +814,14 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         if constexpr (!tb) {
             // per key: (A) is final up to its first denial (inclusive) or its first pending
             // request that is not eligible (exclusive); (D) up to the first state change
-            const uint64_t den = __ballot(pending && elig && !al.allowed) & peers;
+            const uint64_t den = __ballot(pending && elig && (!al.allowed || xs)) & peers;
             const uint64_t nel = __ballot(pending && !elig) & peers;
             const uint32_t fd = den ? (uint32_t)__builtin_ctzll(den) : 64u;
             const uint32_t fs = nel ? (uint32_t)__builtin_ctzll(nel) : 64u;
             fa = fd < fs ? fd : fs;                 // allows: the pending peers below fa
             a_end = fd < fs ? fd + 1u : fs;
+            // (cache) the run's last request is itself an allow when its put sets the entry
+            if (fd < fs && ((__ballot(pending && elig && al.allowed && xs) & peers) >> fd & 1u)) fa = fd + 1u;
             const uint32_t d_end = fm < 64u ? fm + 1u : 64u;
             use_a = a_end > d_end;               // the allow hypothesis decides more
         }
@@ -816,6 +834,9 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                         sw_commit_allows(L, geo, na, nb, nc, (uint32_t)__popcll(ok), q.now_ms);
                         S.sa[slot] = na; S.sb[slot] = nb; S.sc[slot] = nc;
                     }
+                    if constexpr (CACHE)
+                        if (xs && lane + 1u == a_end)        // this request's put sets the entry
+                            S.sx[slot] = (uint64_t)(q.now_ms + L.cache_ttl_ms);
                     r.alw = al.allowed;
                     r.rem = al.remaining;
                     r.tok = __builtin_nan("");

@@ -406,3 +406,22 @@ def test_medium_hot_keys_across_windows(algo):
     got, want, _ = run_both(lims, (keys, permits, now, lim, op), batches=3,
                             capacity=1 << 16)
     assert_same(got, want, "medium-hot")
+
+
+@pytest.mark.parametrize("maxp,start", [(100, 0), (64, 0), (37, 27)])
+def test_sw_local_cache_allow_run_sets_entry(maxp, start):
+    """One key with the cache on: an allow run inside a 64-request group whose last allow's
+    newCount reaches max puts the blocking entry (:119-121); the rest of the window is
+    rejected from the cache (hits), exactly as the reference."""
+    lims = [[rl_amd.SW, maxp, 60_000, 0.0, 0, 1000]]
+    n = 300
+    keys = np.full(n, rl_amd.mix64(np.array([5], np.uint64))[0], np.uint64)
+    t0 = (T0 // 60_000) * 60_000 + 1_000
+    now = ((t0 + start + np.arange(n) // 4) * NS).astype(np.int64)      # 4 requests per ms
+    got, want, e = run_both(lims, (keys, np.ones(n, np.int32), now, np.zeros(n, np.uint16),
+                                   np.zeros(n, np.uint8)), batches=1)
+    assert_same(got, want, "allow run -> cache entry")
+    assert want[0].sum() == maxp
+    o = COracle(lims)
+    o.run(keys, np.ones(n, np.int32), now, np.zeros(n, np.uint16))
+    assert e.stats()["cache_hits"] == o.cache_hits() == n - maxp
