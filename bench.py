@@ -181,8 +181,17 @@ def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remain
     gr = gpu_remaining[:n]
     parity = bool(np.array_equal(ga, a1) and np.array_equal(gr, r1)
                   and np.array_equal(aT, a1) and np.array_equal(rT, r1))
+    cpu_model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {
         "value": n / dtT, "unit": "decisions/s", "cores": threads, "kind": "port",
+        "cpu_model": cpu_model,
         "sample": f"first {n} requests of batch 0 (same synthetic trace), oracle/rl_oracle.c "
                   f"key-sharded over {threads} threads",
         "single_thread_value": n / dt1,
