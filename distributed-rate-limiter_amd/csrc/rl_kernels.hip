@@ -1479,7 +1479,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     };
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0, n_other = 0;
-    uint32_t n_changed = 0, n_tk = 0, n_fb = 0;       // debug: changes, [T0, T1) updates
+    uint32_t n_changed = 0, n_tk = 0, n_fb = 0;       // debug: changes, [T0, T1) updates,
+    uint32_t n_late = 0;                              // detailed chunks starting before T0 / ending past T1
     uint64_t cyc_run = 0, cyc_search = 0, cyc_detail = 0, cyc_pass2 = 0;   // debug stamps
     bool any_hot = false;
     auto pass1 = [&](auto algo) {
@@ -1488,8 +1489,18 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         // [T0, T1) in which every acquire is denied with remaining 0 (whole chunks and groups
         // inside it are decided without being read)
         uint64_t sa = S.sa[hs], sb = S.sb[hs], sc = S.sc[hs];
+        // T1 from the closed-form guess verified at g - 1; when the guess overshoots (the
+        // check fails), the exact first allowed time by a search on the same arithmetic
+        auto t1_of = [&](int64_t t0) {
+            int64_t g = hot_tk_guess<A>(L, t0, sa, sb, sc, 1);
+            if (g > hi + 1) g = hi + 1;
+            if (g <= t0 + 1) return t0;
+            auto pred = [&](int64_t t) { return hot_pred_k<A>(L, t, sa, sb, sc, 1); };
+            if (!pred(g - 1)) return g;
+            return wave_first_true(t0, g - 1, lane, pred);
+        };
         int64_t T0 = hot_t0<A>(lo, hi, sa, sb, sc);
-        int64_t T1 = hot_t1_lb<A>(L, sa, sb, sc, T0, hi);
+        int64_t T1 = t1_of(T0);
         // the hot records of one chunk (lane = arrival order inside the chunk). The next
         // chunk's records are prefetched: undecided chunks come in runs.
         Rec pre = recs[min(f.start + lane, f.end - 1)];
@@ -1555,7 +1566,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         // stays below 1 for a while after an allow), not by another round
                         if (__any(pend)) {
                             T0 = hot_t0<A>(lo, hi, sa, sb, sc);
-                            T1 = hot_t1_lb<A>(L, sa, sb, sc, T0, hi);
+                            T1 = t1_of(T0);
                             t_fresh = true;
                             ++n_tk;
                             const bool fast = q.op == (uint32_t)kOpAcquire && q.now_ms >= T0 && q.now_ms < T1;
@@ -1668,9 +1679,16 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 stale = true;
             } else if (changed || stale) {
                 T0 = hot_t0<A>(lo, hi, sa, sb, sc);
-                T1 = hot_t1_lb<A>(L, sa, sb, sc, T0, hi);
+                T1 = t1_of(T0);
                 ++n_tk;
                 stale = false;
+            } else if (T1 < hi && __any(hot && q.op == (uint32_t)kOpAcquire && q.now_ms >= T1)) {
+                // no change although requests lay past T1: T1 was only a lower bound of the
+                // first allowed time (the guess undershot); without this the chunks up to
+                // the real one would all be read and decided one by one. Exact, from T0.
+                T1 = wave_first_true(T0, hi, lane,
+                                     [&](int64_t t) { return hot_pred_k<A>(L, t, sa, sb, sc, 1); });
+                ++n_tk;
             }
             if (a.dbg) {
                 const uint64_t c_end = __builtin_amdgcn_s_memtime();
@@ -1713,6 +1731,12 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 }
                 if (fst == 64u) break;
                 todo &= fst == 63u ? 0ULL : ~((2ULL << fst) - 1);
+                if (a.dbg) {
+                    const int64_t fmn = (int64_t)readlane64((uint64_t)mn, fst);
+                    const int64_t fmx = (int64_t)readlane64((uint64_t)mx, fst);
+                    n_fb += fmn < T0 ? 1u : 0u;
+                    n_late += fmx >= T1 ? 1u : 0u;
+                }
                 detail(grp * 64 + fst);
             }
         };
@@ -1859,7 +1883,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = f.end - f.start;
             d[3] = (uint64_t)n_detail | (uint64_t)min(n_tk, 0xFFFFu) << 32 | (uint64_t)min(n_fb, 0x7FFFu) << 48 | (1ULL << 63);
             d[4] = cyc_detail; d[5] = cyc_run; d[6] = cyc_search;
-            d[7] = min((uint64_t)n_changed, (uint64_t)0xFFFFFF);
+            d[7] = min((uint64_t)n_changed, (uint64_t)0xFFFFFF) | min((uint64_t)n_late, (uint64_t)0xFFFFFF) << 24;
         }
     }
 }
