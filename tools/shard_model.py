@@ -124,6 +124,9 @@ for s in range(total):
         if bl is not None:
             bl[m:m + cnt] = lim[idx]
         m += cnt
+        # the gathers run on torch's stream, the next slice's synth / partition on the
+        # generator engine's: without this they overwrite keys / now / perm mid-gather
+        torch.cuda.synchronize()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     dec.execute_device(m, bk, bp, bt, bl, None, ba, br)
