@@ -1505,8 +1505,6 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         // chunk's records are prefetched: undecided chunks come in runs.
         Rec pre = recs[min(f.start + lane, f.end - 1)];
         uint32_t pre_c = 0;
-        uint32_t prev_detail = 0xFFFFFFF0u;               // last chunk processed here
-        bool stale = false;                               // [T0, T1) emptied, not recomputed
         auto detail = [&](uint32_t c) {
             ++n_detail;
             const uint64_t c_det = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
@@ -1667,21 +1665,15 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 wave_fence();
                 ++n_changed;
             }
-            // [T0, T1) for the next chunks; none while the key changes state chunk after chunk
-            // (no chunk could be skipped anyway: recomputed after a chunk without a change)
+            // [T0, T1) for the next chunks, after every change (measured: leaving it empty
+            // through runs of changing chunks read the chunk after each of them needlessly)
             const uint64_t c_srch = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-            const bool dense = c == prev_detail + 1;
             if (t_fresh) {
-                stale = false;                            // computed after the last change
-            } else if (changed && dense) {
-                T0 = hot_t0<A>(lo, hi, sa, sb, sc);
-                T1 = T0;
-                stale = true;
-            } else if (changed || stale) {
+                // computed after the last change
+            } else if (changed) {
                 T0 = hot_t0<A>(lo, hi, sa, sb, sc);
                 T1 = t1_of(T0);
                 ++n_tk;
-                stale = false;
             } else if (T1 < hi && __any(hot && q.op == (uint32_t)kOpAcquire && q.now_ms >= T1)) {
                 // no change although requests lay past T1: T1 was only a lower bound of the
                 // first allowed time (the guess undershot); without this the chunks up to
@@ -1699,7 +1691,6 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 put_res<Res>(a, j, oa, orem);
                 if (TOK) a.tok[j] = tk;
             }
-            prev_detail = c;
             if (a.dbg) cyc_detail += __builtin_amdgcn_s_memtime() - c_det;
         };
         // level 1: the chunks of one group of 64

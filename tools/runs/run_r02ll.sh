@@ -1,0 +1,10 @@
+#!/bin/bash
+# validation of the hot-chain change: hot / config / parity GPU tests, then mixed_tenants steady state
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_hot.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_router.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_ll.log 2>&1 || { echo "tests failed"; tail -15 gpurun_out/t_ll.log; exit 1; }
+tail -1 gpurun_out/t_ll.log
+timeout -k 10 300 python -u tools/region_debug.py --config mixed_tenants --batches 6 > gpurun_out/rd_ll.log 2>&1 || { echo "rd failed"; tail -5 gpurun_out/rd_ll.log; exit 1; }
+grep -E "^batch" gpurun_out/rd_ll.log
+timeout -k 10 300 python -u bench.py --config mixed_tenants --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/b_ll.log 2>&1 || { echo "bench failed"; exit 1; }
+tail -1 gpurun_out/b_ll.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('mixed', '%.3e'%d['value'], 'ms/step %.3f'%d['ms_per_step'])"
