@@ -6,14 +6,17 @@ whole hot path (partition -> per-region sequential semantics -> results in calle
 order). Steps are consecutive slices of one synthetic trace, so state carries over
 and time moves forward exactly as in a replay.
 
-Default workload (N=1): BASELINE.json configs[1] — token bucket cap=50, refill=10/s,
-window 60 s (burstRateLimiter, RateLimiterConfig.java:88-92), 1M keys uniform,
-64M-request batches spanning 2 s each.
+Default workload (N=1): BASELINE.json configs[2], the largest single-GPU configuration —
+sliding window 1000/min (SlidingWindowRateLimiter.java:158-180), 100M keys Zipf s=1.1,
+256M-request batches spanning 60 s each. The same JSON line carries configs[1] (token
+bucket cap 50 at 10/s, 1M keys uniform, 64M-request batches; `tb_uniform`) and configs[0]
+(the reference's single-key benchmark; `config1`) as extra keys, each parity-checked.
 
 Multi-GPU (torchrun, one rank per GPU): weak scaling. Every rank is a front-end that
-receives its own 64M-request slice of the global stream; requests are routed to the
-owner shard (top bits of mix64(key)) with RCCL all-to-all, decided there, and the
-decisions return by a second all-to-all.
+receives its own slice of the global stream; requests are routed to the owner shard
+(top bits of mix64(key), or the hot-key directory) by the C-ABI router (rl_router_*,
+the path a JNI caller uses) over RCCL all-to-all, decided there, and the decisions
+return by a second all-to-all.
 """
 from __future__ import annotations
 
@@ -29,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-rate-limiter_amd", "python"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 import rl_amd  # noqa: E402
 
@@ -159,28 +163,45 @@ def config1_line(dev):
                     "tests/cpp/test_host_api (config1)"}
 
 
-def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remaining):
+def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remaining, gpu_tokens,
+                 single_thread=True):
+    """The C oracle (oracle/rl_oracle.c, the CPU restatement: kind "port") on the first
+    sample_n requests of batch 0, key-sharded over the box's host-core share, and (unless
+    single_thread=False) the exact 1-thread replay; both double as the parity check of the
+    GPU's batch 0 on that prefix: decisions, remaining and — token buckets — the fp64
+    balance bit-for-bit (north_star: within 1e-9 relative; Lua TokenBucketRateLimiter.java:56-67)."""
     from oracle.coracle import COracle
     n = min(sample_n, keys.shape[0])
     k = keys[:n].cpu().numpy().view(np.uint64)
     p = permits[:n].cpu().numpy()
     t = now[:n].cpu().numpy()
     l = None if lim is None else lim[:n].cpu().numpy().view(np.uint16)
+    has_tb = any(x[0] == rl_amd.TB for x in cfg["limiters"])
     threads = max(1, min(16, os.cpu_count() or 1))
-    o1 = COracle(cfg["limiters"])
-    t0 = time.perf_counter()
-    a1, r1, _, _ = o1.run(k, p, t, l, None, want_tokens=False)
-    dt1 = time.perf_counter() - t0
-    o1.close()
     oT = COracle(cfg["limiters"], nthreads=threads)
     t0 = time.perf_counter()
-    aT, rT, _, _ = oT.run(k, p, t, l, None, want_tokens=False)
+    aT, rT, tT, _ = oT.run(k, p, t, l, None, want_tokens=has_tb)
     dtT = time.perf_counter() - t0
     oT.close()
+    dt1 = None
+    if single_thread:
+        o1 = COracle(cfg["limiters"])
+        t0 = time.perf_counter()
+        a1, r1, _, _ = o1.run(k, p, t, l, None, want_tokens=False)
+        dt1 = time.perf_counter() - t0
+        o1.close()
+        ok_1 = bool(np.array_equal(aT, a1) and np.array_equal(rT, r1))
+    else:
+        ok_1 = True
     ga = gpu_allowed[:n]
     gr = gpu_remaining[:n]
-    parity = bool(np.array_equal(ga, a1) and np.array_equal(gr, r1)
-                  and np.array_equal(aT, a1) and np.array_equal(rT, r1))
+    dec_ok = bool(np.array_equal(ga, aT) and np.array_equal(gr, rT)) and ok_1
+    bal = None
+    if has_tb:
+        gt = gpu_tokens[:n]
+        m = ~np.isnan(tT)
+        bal = bool(np.array_equal(np.isnan(gt), ~m) and
+                   np.array_equal(gt[m].view(np.uint64), tT[m].view(np.uint64)))
     cpu_model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -189,75 +210,28 @@ def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remain
                 break
     except OSError:
         pass
-    return {
+    out = {
         "value": n / dtT, "unit": "decisions/s", "cores": threads, "kind": "port",
         "cpu_model": cpu_model,
         "sample": f"first {n} requests of batch 0 (same synthetic trace), oracle/rl_oracle.c "
                   f"key-sharded over {threads} threads",
-        "single_thread_value": n / dt1,
-        "single_thread_seconds": dt1,
         "sharded_seconds": dtT,
-    }, parity, n
+    }
+    if dt1 is not None:
+        out["single_thread_value"] = n / dt1
+        out["single_thread_seconds"] = dt1
+    return out, dec_ok, bal, n
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="tb_uniform", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=0, help="requests per GPU per step (override)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 26)
-    ap.add_argument("--tune", action="append", default=[],
-                    help="engine knob key=value (rl_tune), e.g. bin_shift=0")
-    ap.add_argument("--table-scale", type=int, default=1,
-                    help="size the state tables for this many times the config's key count "
-                         "(engine sizing: lower load, more and smaller regions)")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="N=1: overlap batch s+1's partition with batch s's decisions (RL_OPT_PIPELINE)")
-    ap.add_argument("--stage-timing", action="store_true",
-                    help="also record hipEvents inside the timed steps (diagnostics only)")
-    args = ap.parse_args()
+def parity_text(dec_ok, bal, n):
+    s = f"{'bit-exact' if dec_ok else 'MISMATCH'} decisions + remaining vs oracle on the first {n} " \
+        f"requests of batch 0"
+    if bal is not None:
+        s += f"; token-bucket balances {'bit-exact' if bal else 'MISMATCH'}"
+    return s
 
-    ws, rank, local = dist_env()
-    if ws != args.gpus and not (ws == 1 and args.gpus == 1):
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
-    # RL_BENCH_REHEARSE=1: every rank on cuda:0, exchanges through gloo on the host — a
-    # functional rehearsal of the N>1 path on a one-GPU box (its numbers mean nothing)
-    rehearse = ws > 1 and os.environ.get("RL_BENCH_REHEARSE") == "1"
-    if rehearse:
-        local = 0
-    torch.cuda.set_device(local)
-    if ws > 1:
-        import torch.distributed as dist
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    cfg = CONFIGS[args.config]
-    n = args.batch or cfg["batch"]
-    steps, warm = args.steps, args.warmup
-    total_steps = steps + warm
 
-    # weak scaling: each shard owns 1/ws of the keys but sees ws x n requests' worth of
-    # key space across ranks, i.e. the same number of requests per GPU; a shard's table
-    # is sized for its share of the global key population.
-    # an owner can receive up to ws x n requests in a skewed step (the router grows its
-    # receive buffers; the engine's scratch is allocated for what it actually receives)
-    # --pipeline (N=1): RL_OPT_PIPELINE, batch s+1's partition on a second stream while batch s's
-    # decisions are applied; measured slower on tb_uniform, so off by default
-    eng = rl_amd.Engine(device=local, max_batch=n * ws,
-                        capacity=cfg["capacity"] * ws * args.table_scale, stage_timing=False,
-                        shard_index=rank,
-                        shard_count=ws, pipeline=ws == 1 and args.pipeline)
-    for l in cfg["limiters"]:
-        eng.add_limiter(*l)
-    for kv in args.tune:
-        k, v = kv.split("=")
-        eng.tune(k, int(v))
-
-    dev = torch.device("cuda", local)
+def make_inputs(eng, cfg, n, ws, rank, total_steps, dev):
     n_global_total = total_steps * ws * n
     n_lim = len(cfg["limiters"])
     inputs = []
@@ -272,39 +246,92 @@ def main():
                         span_ns=cfg["span_ns"] * total_steps,
                         index_base=(s * ws + rank) * n, n_total=n_global_total, n_limiters=n_lim)
         inputs.append((keys, permits, now, lim))
+    return inputs
+
+
+def plan_directory(router, cfg, inputs, n, k=4096, sample=1 << 22):
+    """Hot-key directory (rl_router_plan_directory) from this rank's first batch: the top
+    keys of a sample of its requests (Zipf configs; BASELINE north_star's skew)."""
+    keys = inputs[0][0][:min(sample, n)]
+    u, c = torch.unique(keys, return_counts=True)
+    top = torch.topk(c, min(k, c.numel()))
+    kk = u[top.indices].cpu().numpy().view(np.uint64)
+    cc = top.values.cpu().numpy().astype(np.uint64)
+    return router.plan_directory(kk, cc, int(keys.numel()), k)
+
+
+def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
+    """Time `steps` steps of config `name` after `warm` warmup steps; returns the line's
+    dict and what the CPU baseline needs (batch 0's inputs and GPU results)."""
+    cfg = CONFIGS[name]
+    n = (args.batch if name == args.config else 0) or cfg["batch"]
+    total_steps = steps + warm
+    # weak scaling: each shard owns 1/ws of the keys but sees ws x n requests' worth of
+    # key space across ranks, i.e. the same number of requests per GPU; a shard's table
+    # is sized for its share of the global key population. An owner can receive up to
+    # ws x n requests in a skewed step.
+    eng = rl_amd.Engine(device=local, max_batch=n * ws,
+                        capacity=cfg["capacity"] * ws * args.table_scale, stage_timing=False,
+                        shard_index=rank, shard_count=ws,
+                        pipeline=ws == 1 and args.pipeline)
+    for l in cfg["limiters"]:
+        eng.add_limiter(*l)
+    for kv in args.tune:
+        k, v = kv.split("=")
+        eng.tune(k, int(v))
+    n_lim = len(cfg["limiters"])
+    inputs = make_inputs(eng, cfg, n, ws, rank, total_steps, dev)
     allowed = torch.empty(n, dtype=torch.uint8, device=dev)
     remaining = torch.empty(n, dtype=torch.int64, device=dev)
+    has_tb = any(x[0] == rl_amd.TB for x in cfg["limiters"])
+    tokens0 = torch.empty(n, dtype=torch.float64, device=dev) if (parity_tokens and has_tb) else None
     eng.sync()
     torch.cuda.synchronize()
 
+    router = None
+    directory = 0
     if ws > 1:
-        from rl_amd.router import DeviceOps, Router
-        router = Router(DeviceOps(eng, ws, dev, n), ws, rank,
-                        exchange_device="cpu" if rehearse else None)
+        if args.router == "python":
+            from rl_amd.router import DeviceOps, Router
+            router = Router(DeviceOps(eng, ws, dev, n), ws, rank,
+                            exchange_device="cpu" if rehearse else None)
 
-        def step(s):
-            k, p, t, li = inputs[s]
-            router.step(k, p, t, allowed, remaining, li)
+            def step(s, tok=None):
+                k, p, t, li = inputs[s]
+                router.step(k, p, t, allowed, remaining, li)
+        else:
+            from rl_amd.capi_router import CRouter
+            router = CRouter(eng, ws, rank, n, transport="host" if rehearse else "rccl",
+                             device=local)
+            if cfg["dist"] == rl_amd.DIST_ZIPF and not args.no_directory:
+                directory = plan_directory(router, cfg, inputs, n)
+
+            def step(s, tok=None):
+                k, p, t, li = inputs[s]
+                router.step(n, k, p, t, li, allowed, remaining)
     else:
-        def step(s):
+        def step(s, tok=None):
             k, p, t, li = inputs[s]
-            eng.execute_device(n, k, p, t, li, None, allowed, remaining)
+            eng.execute_device(n, k, p, t, li, None, allowed, remaining, tok)
 
-    # Warmup steps. Steps 1.. of the warmup carry hipEvents between the stages (the
-    # per-stage breakdown); the timed steps below run without them.
+    # Warmup steps. Step 0 also returns the TB balances (parity); steps 1.. of the warmup
+    # carry hipEvents between the stages (the per-stage breakdown); the timed steps below
+    # run without them.
     keep0 = None
     stages = {}
     for s in range(warm):
         if s == 1:
             eng.tune("stage_timing", 1)
-        step(s)
+        step(s, tokens0 if s == 0 else None)
         if s == 0:
             eng.sync()
-            keep0 = (allowed.cpu().numpy(), remaining.cpu().numpy())
+            torch.cuda.synchronize()
+            keep0 = (allowed.cpu().numpy(), remaining.cpu().numpy(),
+                     None if tokens0 is None else tokens0.cpu().numpy())
     if warm > 1:
         stages = eng.stage_times()
     eng.tune("stage_timing", 1 if args.stage_timing else 0)
-    st = eng.last_status()
+    del tokens0
 
     if ws > 1:
         dist.barrier()
@@ -319,7 +346,6 @@ def main():
     elapsed = time.perf_counter() - t0
     if ws > 1:
         router.finish()                    # collective: raises on every rank on an engine error
-    if ws > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -336,13 +362,12 @@ def main():
         for k in ("upsweep1", "scan1", "scatter1"):
             kern.pop(k, None)
     U = stats["distinct_keys"]
-    n_lim = len(cfg["limiters"])
     req_bytes = REQ_IN + (2 if n_lim > 1 else 0) + REQ_OUT
     algo_bytes = n * req_bytes + U * KEY_BYTES            # per GPU per step
     step_s = elapsed / steps
     achieved = algo_bytes * ws / step_s / 1e9             # whole node
     peak = HBM_PEAK_GBS * ws
-    traffic = load_pmc(args.config, "step")
+    traffic = load_pmc(name, "step")
     res_b = eng.result_width()
     kernels = {}
     for k, ms in kern.items():
@@ -350,7 +375,6 @@ def main():
         kernels[k] = {"ms": round(ms, 4), "io_bytes": io,
                       "io_frac": None if io is None else round(io / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     dom = max(kern, key=kern.get) if kern else None
-
     out = {
         "metric": "rate-limit decisions/sec (whole node)",
         "value": value,
@@ -362,11 +386,16 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64" if all(l[0] == rl_amd.TB for l in cfg["limiters"]) else "int64+f64",
+        "dtype": "f64" if all(l[0] == rl_amd.TB for l in cfg["limiters"]) else
+                 ("int64" if not has_tb else "int64+f64"),
         "data": "synthetic (deterministic splitmix64 trace generated on device)",
-        "config": {"workload": f"{args.config}: {cfg['desc']}", "requests_per_gpu_per_step": n,
-                   "n_keys": cfg["n_keys"] * ws, "n_limiters": n_lim, "parallelism": f"key-hash shards x{ws}"
-                   + (" + RCCL all-to-all routing" if ws > 1 else "")},
+        "config": {"workload": f"{name}: {cfg['desc']}", "requests_per_gpu_per_step": n,
+                   "n_keys": cfg["n_keys"] * ws, "n_limiters": n_lim,
+                   "parallelism": f"key-hash shards x{ws}"
+                   + (f" + {'C-ABI rl_router' if args.router == 'capi' else 'python router'} "
+                      f"all-to-all ({'host rehearsal' if rehearse else 'RCCL'})"
+                      + (f", hot-key directory {directory} keys" if directory else "")
+                      if ws > 1 else "")},
         # Headline: the whole step's ALGORITHMIC bytes (N x (in + out) + U x
         # (slot read + write)) over the whole step's wall time, against 8 TB/s per GPU. The
         # step is one launch sequence of the pipeline kernels; `kernels` breaks it down.
@@ -380,15 +409,81 @@ def main():
                                               "capacity_errors", "regions_touched")},
         "status": rl_amd.strerror(st),
     }
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        k0, p0, t0_, l0 = inputs[0]
-        cb, parity, m = cpu_baseline(cfg, k0, p0, t0_, l0, args.cpu_sample, keep0[0], keep0[1])
+    if router is not None and hasattr(router, "close"):
+        router.close()
+    eng.close()
+    return out, inputs[0], keep0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="sw_zipf", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="requests per GPU per step (override)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="N=1: skip the extra tb_uniform / config1 keys of the line")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 26)
+    ap.add_argument("--tune", action="append", default=[],
+                    help="engine knob key=value (rl_tune), e.g. bin_shift=0")
+    ap.add_argument("--table-scale", type=int, default=1,
+                    help="size the state tables for this many times the config's key count "
+                         "(engine sizing: lower load, more and smaller regions)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="N=1: overlap batch s+1's partition with batch s's decisions (RL_OPT_PIPELINE)")
+    ap.add_argument("--stage-timing", action="store_true",
+                    help="also record hipEvents inside the timed steps (diagnostics only)")
+    ap.add_argument("--router", choices=("capi", "python"), default="capi",
+                    help="N>1: the C-ABI router (product path) or the torch.distributed one")
+    ap.add_argument("--no-directory", action="store_true",
+                    help="N>1: hash owners only (no hot-key directory on Zipf configs)")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    if ws != args.gpus and not (ws == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+    # RL_BENCH_REHEARSE=1: every rank on cuda:0, exchanges through gloo on the host — a
+    # functional rehearsal of the N>1 path on a one-GPU box (its numbers mean nothing)
+    rehearse = ws > 1 and os.environ.get("RL_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
+    torch.cuda.set_device(local)
+    if ws > 1:
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    baseline = rank == 0 and ws == 1 and not args.no_cpu_baseline
+    out, in0, keep0 = run(args.config, args, ws, rank, local, dev, rehearse, args.steps,
+                          args.warmup, parity_tokens=baseline)
+    if baseline:
+        k0, p0, t0_, l0 = in0
+        cb, dec_ok, bal, m = cpu_baseline(CONFIGS[args.config], k0, p0, t0_, l0, args.cpu_sample,
+                                          keep0[0], keep0[1], keep0[2])
         out["cpu_baseline"] = cb
-        out["parity"] = f"{'bit-exact' if parity else 'MISMATCH'} vs oracle on the first {m} " \
-                        f"requests of batch 0"
-        out["config1"] = config1_line(dev)
+        out["parity"] = parity_text(dec_ok, bal, m)
     else:
         out["cpu_baseline"] = None
+    del in0
+    if baseline and not args.no_extra:
+        torch.cuda.empty_cache()
+        if args.config != "tb_uniform":
+            # BASELINE configs[1] on the same box: the token-bucket line, parity incl. balances
+            tb, tin0, tkeep0 = run("tb_uniform", args, 1, 0, local, dev, False, args.steps,
+                                   args.warmup, parity_tokens=True)
+            cbt, dec_t, bal_t, mt = cpu_baseline(CONFIGS["tb_uniform"], *tin0, args.cpu_sample,
+                                                 tkeep0[0], tkeep0[1], tkeep0[2], single_thread=False)
+            out["tb_uniform"] = {k: tb[k] for k in ("value", "unit", "ms_per_step", "config", "stage_ms",
+                                                    "batch_stats", "status")}
+            out["tb_uniform"]["roofline_frac"] = tb["roofline"]["frac"]
+            out["tb_uniform"]["cpu_baseline"] = cbt
+            out["tb_uniform"]["parity"] = parity_text(dec_t, bal_t, mt)
+            del tin0
+            torch.cuda.empty_cache()
+        out["config1"] = config1_line(dev)
     if rank == 0:
         print(json.dumps(out))
     if ws > 1:

@@ -101,7 +101,7 @@ struct rl_engine {
     uint32_t region_walk = 0;               // rl_tune("region_walk"): persistent waves per CU
     uint32_t* d_work = nullptr;             // its claim counters (8 x 64 B)
     // hot regions
-    uint32_t* hot_list = nullptr;           // [kHotMax + 40]: list, k_hot_select's meta, total
+    uint32_t* hot_list = nullptr;           // [kHotListWords]: list, k_hot_select's meta, totals
     HotInfo* hot_info = nullptr;            // [kHotMax]
     uint64_t* hot_summ = nullptr;           // [hot_summ_cap][4]
     size_t hot_summ_cap = 0, hot_summ_l1 = 0;
@@ -238,7 +238,13 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
         rl_destroy(e);
         return RL_E_DEVICE;
     }
-    if (hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess ||
+    // The hot chains' stream has the device's highest priority: their workgroups are a few
+    // long sequential critical paths launched beside ~10^5-10^6 short normal-region waves,
+    // and at equal priority the dispatcher interleaved the two launches, so some chains
+    // only started once normal regions had drained (sw_zipf: up to 2.5 ms late).
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+    if (hipStreamCreateWithPriority(&e->hstream, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
         hipEventCreateWithFlags(&e->hot_ev[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->hot_ev[1], hipEventDisableTiming) != hipSuccess) {
         rl_destroy(e);
@@ -271,7 +277,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
         rc = RL_E_DEVICE;
     if (rc == RL_OK && hipHostMalloc((void**)&e->h_ctl, sizeof(BatchCtl)) != hipSuccess) rc = RL_E_NOMEM;
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
-    if (rc == RL_OK) rc = dalloc(&e->hot_list, kHotMax + 40);
+    if (rc == RL_OK) rc = dalloc(&e->hot_list, kHotListWords);
     if (rc == RL_OK) rc = dalloc(&e->hot_info, kHotMax);
     if (rc != RL_OK) { rl_destroy(e); return rc; }
     std::memset(e->h_ctl, 0, sizeof(BatchCtl));
@@ -684,13 +690,13 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     if (hot) {
         uint32_t* hot_count = e->hot_list + kHotMax;
-        HIP_OK(hipMemsetAsync(hot_count, 0, 34 * sizeof(uint32_t), s));
+        HIP_OK(hipMemsetAsync(hot_count, 0, kHotMetaWords * sizeof(uint32_t), s));
         HIP_OK(launch_hot_select(rstart, rcount, rend, n_bins, e->hot_threshold, e->hot_list,
                                  hot_count, e->hot_mark, e->epoch, s));
         ra.hot_list = e->hot_list; ra.hot_count = hot_count; ra.hot_mark = e->hot_mark;
         ra.epoch = e->epoch;
         ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ;
-        ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 4; ra.hot_total = e->hot_list + kHotMax + 36;
+        ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 4; ra.hot_total = e->hot_list + kHotMax + kHotTotalOff;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
     }
     mark(e, 7);
@@ -1115,6 +1121,25 @@ extern "C" int rl_route_pack_wire(rl_engine* e, size_t n, const uint32_t* perm, 
                                   limiter_out, hdr, s));
     return RL_OK;
 }
+
+namespace rl {
+// rl_route_pack_wire plus the per-block now_ms min / max partials of the router's header
+// (internal: rl_router.cpp).
+int route_pack_wire_mm(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key,
+                       const int32_t* permits, const int64_t* now_ns, const uint16_t* limiter,
+                       uint64_t* wire_out, uint16_t* limiter_out, int64_t* hdr, uint64_t* part,
+                       uint32_t* nparts, void* stream) {
+    if (!e || !hdr || !part || !nparts || (n && (!perm || !key || !permits || !now_ns || !wire_out)))
+        return RL_E_INVALID_ARG;
+    if (n > 0xFFFFFFF0ULL) return RL_E_TOO_LARGE;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_OK(launch_route_pack_wire((uint32_t)n, perm, key, permits, now_ns, limiter, wire_out,
+                                  limiter_out, hdr, s, part, nparts));
+    return RL_OK;
+}
+int engine_device(rl_engine* e) { return e ? e->device : 0; }
+}  // namespace rl
 
 extern "C" int rl_route_unwire(rl_engine* e, size_t m, const uint64_t* wire, uint32_t n_src,
                                const int64_t* src_base, const uint64_t* src_count,

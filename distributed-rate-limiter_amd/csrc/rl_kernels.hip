@@ -1795,29 +1795,57 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 count -= 64;
             }
         };
-        for (uint32_t g0 = 0; g0 < f.n_groups; g0 += 64) {
+        // The chunks holding other keys' records, in arrival order, across groups: a
+        // wave-uniform cursor over (block of 64 groups, group, chunk). Four chunks' records
+        // are in flight (unrolled, so the prefetch registers rotate without moves): a region
+        // whose second key is itself hot runs thousands of chunks through here, and one
+        // chunk in flight left each of them waiting on its load (sw_zipf: a 398K-record
+        // region ended the region stage 3.5 ms after the normal regions).
+        uint32_t cg0 = 0, cgrp = 0;
+        uint64_t cgtodo = 0, ctodo = 0;
+        bool cdone = f.n_groups == 0;
+        auto group_mask = [&](uint32_t g0) {
             const uint32_t g = g0 + lane;
-            const bool gho = g < f.n_groups && (!hot_ok || ((grp_at(g)[3] >> 8) & 1u));
-            uint64_t gtodo = __ballot(gho);
-            while (gtodo) {
-                const uint32_t grp = g0 + (uint32_t)__builtin_ctzll(gtodo);
-                gtodo &= gtodo - 1;
-                const uint32_t c = grp * 64 + lane;
+            return __ballot(g < f.n_groups && (!hot_ok || ((grp_at(g)[3] >> 8) & 1u)));
+        };
+        if (!cdone) cgtodo = group_mask(0);
+        auto next_chunk = [&]() -> uint32_t {
+            while (!cdone && ctodo == 0) {
+                if (cgtodo == 0) {
+                    cg0 += 64;
+                    if (cg0 >= f.n_groups) { cdone = true; break; }
+                    cgtodo = group_mask(cg0);
+                    continue;
+                }
+                cgrp = cg0 + (uint32_t)__builtin_ctzll(cgtodo);
+                cgtodo &= cgtodo - 1;
+                const uint32_t c = cgrp * 64 + lane;
                 uint32_t no = 0;
                 if (c < f.n_chunks) no = hot_ok ? (uint32_t)(summ_at(c)[3] >> 8) & 0xFFu : 64u;
-                uint64_t todo = __ballot(no != 0);
-                // the chunks with other keys' records, the next one's records in flight
-                auto rec_of = [&](uint32_t cc) { return recs[min(f.start + cc * kHotChunk + lane, f.end - 1)]; };
-                Rec nxt = todo ? rec_of(grp * 64 + (uint32_t)__builtin_ctzll(todo)) : Rec{};
-                while (todo) {
-                    const uint32_t cc = grp * 64 + (uint32_t)__builtin_ctzll(todo);
-                    todo &= todo - 1;
-                    const Rec r = nxt;
-                    if (todo) nxt = rec_of(grp * 64 + (uint32_t)__builtin_ctzll(todo));
-                    const uint32_t j = f.start + cc * kHotChunk + lane;
-                    take(r, j, j < f.end);
-                }
+                ctodo = __ballot(no != 0);
             }
+            if (cdone) return kNone;
+            const uint32_t cc = cgrp * 64 + (uint32_t)__builtin_ctzll(ctodo);
+            ctodo &= ctodo - 1;
+            return cc;
+        };
+        auto rec_of = [&](uint32_t cc) {
+            return recs[cc == kNone ? f.start : min(f.start + cc * kHotChunk + lane, f.end - 1)];
+        };
+        auto take_chunk = [&](const Rec& r, uint32_t cc) {
+            const uint32_t j = f.start + cc * kHotChunk + lane;
+            take(r, j, j < f.end);
+        };
+        uint32_t k0 = next_chunk(), k1 = next_chunk(), k2 = next_chunk(), k3 = next_chunk();
+        Rec r0 = rec_of(k0), r1 = rec_of(k1), r2 = rec_of(k2), r3 = rec_of(k3);
+        while (k0 != kNone) {
+            take_chunk(r0, k0); k0 = next_chunk(); r0 = rec_of(k0);
+            if (k1 == kNone) break;
+            take_chunk(r1, k1); k1 = next_chunk(); r1 = rec_of(k1);
+            if (k2 == kNone) break;
+            take_chunk(r2, k2); k2 = next_chunk(); r2 = rec_of(k2);
+            if (k3 == kNone) break;
+            take_chunk(r3, k3); k3 = next_chunk(); r3 = rec_of(k3);
         }
         if (count > 0) apply64(count);
         if (a.dbg) cyc_pass2 += __builtin_amdgcn_s_memtime() - c_p2;
@@ -2017,9 +2045,11 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
                                                     uint32_t* hot_meta, uint32_t* hot_mark,
                                                     uint32_t epoch) {
     __shared__ uint32_t s_thr;
+    __shared__ uint32_t s_off[33];                    // list offset of each size class
     if (threadIdx.x == 0) {
         uint32_t above = 0, thr = 0xFFFFFFFFu;
         for (int c = 32; c >= 0; --c) {               // classes from the largest down
+            s_off[c] = above;
             above += hot_meta[1 + c];
             if (above > kHotMax) break;
             thr = c == 0 ? 1u : (1u << c);
@@ -2031,7 +2061,11 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
     if (b >= n_bins) return;
     const uint32_t cnt = bin_records(rstart, rcount, rend, b);
     if (cnt == 0 || cnt < s_thr) return;
-    const uint32_t k = atomicAdd(&hot_meta[0], 1u);
+    // largest size class first: the chains' workgroups are dispatched in list order, and the
+    // longest chains must not be the ones that wait for a slot beside the normal regions
+    const uint32_t c = 31u - (uint32_t)__builtin_clz(cnt);
+    const uint32_t k = s_off[c] + atomicAdd(&hot_meta[kHotClassCursor + c], 1u);
+    atomicAdd(&hot_meta[0], 1u);
     if (k < kHotMax) {                                // (always, by the choice of s_thr)
         hot_list[k] = b;
         hot_mark[b] = epoch;
@@ -2394,15 +2428,23 @@ __global__ __launch_bounds__(256) void k_route_pack_wire(uint32_t n, const uint3
                                                          const uint16_t* __restrict__ lim,
                                                          uint64_t* __restrict__ wire,
                                                          uint16_t* __restrict__ lim_o,
-                                                         int64_t* __restrict__ hdr) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+                                                         int64_t* __restrict__ hdr,
+                                                         uint64_t* __restrict__ part) {
+    // grid-stride (a capped grid): with `part`, block b leaves the ordered-key min / max of
+    // its requests' now_ms in part[2b], part[2b+1] (the router's header reduces them; no
+    // atomics on one word, which sustains only ~88 adds per us)
     const int64_t base = floor_div_ms(now[0]) - (1LL << 31);
-    if (j == 0) hdr[0] = base;
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = base;
     bool bad = false;
-    if (j < n) {
+    uint64_t mn = ~0ULL, mx = 0;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
         const uint32_t i = perm[j];
-        const int64_t rel = floor_div_ms(now[i]) - base;
-        bad = rel < 0 || rel > 0xFFFFFFFFLL;
+        const int64_t ms = floor_div_ms(now[i]);
+        const int64_t rel = ms - base;
+        bad |= rel < 0 || rel > 0xFFFFFFFFLL;
+        const uint64_t k = ord_key(ms);
+        mn = k < mn ? k : mn;
+        mx = k > mx ? k : mx;
         ulonglong2 w;
         w.x = key[i];
         w.y = (uint64_t)(uint32_t)permits[i] << 32 | (uint64_t)(uint32_t)rel;
@@ -2410,7 +2452,27 @@ __global__ __launch_bounds__(256) void k_route_pack_wire(uint32_t n, const uint3
         if (lim_o) lim_o[j] = lim ? lim[i] : 0;
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&hdr[1], 1ULL);
+    if (part) {
+        __shared__ uint64_t s_mm[2][4];
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        const uint32_t w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0) { s_mm[0][w] = mn; s_mm[1][w] = mx; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t k = 1; k < blockDim.x / 64; ++k) {
+                mn = s_mm[0][k] < mn ? s_mm[0][k] : mn;
+                mx = s_mm[1][k] > mx ? s_mm[1][k] : mx;
+            }
+            part[2 * blockIdx.x] = mn;
+            part[2 * blockIdx.x + 1] = mx;
+        }
+    }
 }
+
 
 struct WireSrc {                 // receiver: source s holds requests [end[s-1], end[s])
     int64_t base[kMaxShards];
@@ -2582,19 +2644,59 @@ __global__ void k_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* 
     if (t < g) hdr[(size_t)t * stride] = counts[t];
 }
 
-// Router header rows {count (already there), base_ms, overflow, published status}.
-__global__ void k_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, uint32_t g) {
+// Router header rows (kHdrWords int64 each): {count (already there), base_ms, overflow,
+// published status, capacity, min now_ms, max now_ms, 0}; min / max folded from
+// k_route_pack_wire's per-block partials (nparts = 0: an empty batch, min > max).
+__global__ __launch_bounds__(256) void k_fill_header(int64_t* hdr, const int64_t* base_ovf,
+                                                     int64_t status, int64_t cap, uint32_t g,
+                                                     const uint64_t* part, uint32_t nparts) {
+    __shared__ uint64_t s_mm[2][4];
     const uint32_t t = threadIdx.x;
+    uint64_t mn = ~0ULL, mx = 0;
+    for (uint32_t b = t; b < nparts; b += 256) {
+        mn = part[2 * b] < mn ? part[2 * b] : mn;
+        mx = part[2 * b + 1] > mx ? part[2 * b + 1] : mx;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if ((t & 63) == 0) { s_mm[0][t >> 6] = mn; s_mm[1][t >> 6] = mx; }
+    __syncthreads();
+    for (int k = 0; k < 4; ++k) {
+        mn = s_mm[0][k] < mn ? s_mm[0][k] : mn;
+        mx = s_mm[1][k] > mx ? s_mm[1][k] : mx;
+    }
     if (t < g) {
-        hdr[(size_t)t * 4 + 1] = base_ovf[0];
-        hdr[(size_t)t * 4 + 2] = base_ovf[1];
-        hdr[(size_t)t * 4 + 3] = status;
+        int64_t* row = hdr + (size_t)t * kHdrWords;
+        row[1] = base_ovf[0];
+        row[2] = base_ovf[1];
+        row[3] = status;
+        row[4] = cap;
+        row[5] = mn == ~0ULL ? INT64_MAX : (int64_t)(mn ^ 0x8000000000000000ULL);
+        row[6] = mx == 0ULL ? INT64_MIN : (int64_t)(mx ^ 0x8000000000000000ULL);
+        row[7] = 0;
     }
 }
 
-hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, uint32_t g,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(k_fill_header, dim3(1), dim3(64), 0, s, hdr, base_ovf, status, g);
+hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, int64_t cap,
+                              uint32_t g, const uint64_t* part, uint32_t nparts, hipStream_t s) {
+    hipLaunchKernelGGL(k_fill_header, dim3(1), dim3(256), 0, s, hdr, base_ovf, status, cap, g, part,
+                       nparts);
+    return hipGetLastError();
+}
+
+// Requests not decided (a router step whose engine call failed): allowed 0, remaining `rem`.
+__global__ void k_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, int64_t rem) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { allowed[i] = 0; remaining[i] = rem; }
+}
+
+hipError_t launch_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, int64_t rem,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_value, dim3((n + 255) / 256), dim3(256), 0, s, allowed, remaining, n, rem);
     return hipGetLastError();
 }
 
@@ -3095,11 +3197,15 @@ hipError_t launch_route_unpack(uint32_t n, const uint32_t* perm, const int64_t* 
 
 hipError_t launch_route_pack_wire(uint32_t n, const uint32_t* perm, const uint64_t* key,
                                   const int32_t* permits, const int64_t* now, const uint16_t* lim,
-                                  uint64_t* wire, uint16_t* lim_o, int64_t* hdr, hipStream_t s) {
+                                  uint64_t* wire, uint16_t* lim_o, int64_t* hdr, hipStream_t s,
+                                  uint64_t* part, uint32_t* nparts) {
+    if (nparts) *nparts = 0;
     hipError_t e = hipMemsetAsync(hdr, 0, 2 * sizeof(int64_t), s);
     if (e != hipSuccess || n == 0) return e;
-    hipLaunchKernelGGL(k_route_pack_wire, dim3((n + 255) / 256), dim3(256), 0, s, n, perm, key,
-                       permits, now, lim, wire, lim_o, hdr);
+    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, kWireBlocksMax);
+    if (nparts) *nparts = blocks;
+    hipLaunchKernelGGL(k_route_pack_wire, dim3(blocks), dim3(256), 0, s, n, perm, key,
+                       permits, now, lim, wire, lim_o, hdr, part);
     return hipGetLastError();
 }
 

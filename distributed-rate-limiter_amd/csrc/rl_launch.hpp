@@ -5,6 +5,8 @@
 
 #include "rl_device.hpp"
 
+struct rl_engine;   // include/rl_engine.h
+
 namespace rl {
 
 // Ablation bits (rl_tune "ablate"): timing experiments only; results are wrong when set.
@@ -121,6 +123,13 @@ constexpr uint32_t kDirMax = 4096;
 constexpr uint32_t kDirEmpty = 0xFFFFFFFFu;
 struct DirSlot { uint64_t tag; uint32_t owner; uint32_t pad; };
 constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
+// hot_list layout: [kHotMax] list, then the selection's meta words: [0] listed count,
+// [1 .. 33] size-class histogram, [kHotClassCursor ..+33] per-class list cursors, then
+// [kHotTotalOff .. +2] chunk / group totals (k_hot_scan).
+constexpr uint32_t kHotClassCursor = 34;
+constexpr uint32_t kHotMetaWords = 68;   // zeroed before every batch
+constexpr uint32_t kHotTotalOff = 68;
+constexpr uint32_t kHotListWords = kHotMax + 72;
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
 constexpr uint32_t kDbgWords = 8;        // debug words per bin
 // Batch counters are sharded: one device-scope atomic word sustains only ~88 adds per us
@@ -262,9 +271,13 @@ hipError_t launch_route_fold(uint32_t n, const uint8_t* allowed, const int64_t* 
                              int64_t* packed, hipStream_t s);
 hipError_t launch_route_unpack(uint32_t n, const uint32_t* perm, const int64_t* packed,
                                uint8_t* allowed, int64_t* remaining, hipStream_t s);
+// part (nullable, >= 2 * kWireBlocksMax u64): per-block now_ms min / max partials for the
+// router header; *nparts (nullable) = blocks launched.
+constexpr uint32_t kWireBlocksMax = 2048;
 hipError_t launch_route_pack_wire(uint32_t n, const uint32_t* perm, const uint64_t* key,
                                   const int32_t* permits, const int64_t* now, const uint16_t* lim,
-                                  uint64_t* wire, uint16_t* lim_o, int64_t* hdr, hipStream_t s);
+                                  uint64_t* wire, uint16_t* lim_o, int64_t* hdr, hipStream_t s,
+                                  uint64_t* part = nullptr, uint32_t* nparts = nullptr);
 hipError_t launch_route_unwire(uint32_t m, const uint64_t* wire, uint32_t n_src, const int64_t* base,
                                const uint32_t* end, uint64_t* key_o, int32_t* permits_o,
                                int64_t* now_o, hipStream_t s);
@@ -296,7 +309,18 @@ hipError_t launch_route_unpack_ret(uint32_t n, const uint32_t* perm, const void*
                                    hipStream_t s);
 hipError_t launch_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride,
                                    hipStream_t s);
-hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, uint32_t g,
-                              hipStream_t s);
+// Router header: kHdrWords int64 per peer row.
+constexpr uint32_t kHdrWords = 8;
+hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, int64_t cap,
+                              uint32_t g, const uint64_t* part, uint32_t nparts, hipStream_t s);
+hipError_t launch_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, int64_t rem,
+                             hipStream_t s);
+
+// internal helpers of rl_engine.cpp for rl_router.cpp (not part of the C-ABI)
+int route_pack_wire_mm(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key,
+                       const int32_t* permits, const int64_t* now_ns, const uint16_t* limiter,
+                       uint64_t* wire_out, uint16_t* limiter_out, int64_t* hdr, uint64_t* part,
+                       uint32_t* nparts, void* stream);
+int engine_device(rl_engine* e);
 
 }  // namespace rl

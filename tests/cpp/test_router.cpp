@@ -117,7 +117,8 @@ static const int64_t kLims[2][3] = {{1, 50, 60000}, {0, 30, 5000}};   // TB 50 @
 static const double kRefill[2] = {10.0, 0.0};
 
 static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int steps, bool dir,
-                     uint64_t capacity, Result* out, rl_transport* ext_t = nullptr) {
+                     uint64_t capacity, Result* out, rl_transport* ext_t = nullptr,
+                     bool nosync_finish = false) {
     HIPC(hipSetDevice(0));
     rl_opts o{};
     o.device = 0; o.max_batch = (uint64_t)G * n; o.default_capacity = capacity;
@@ -163,11 +164,14 @@ static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int
         HIPC(hipMemcpyAsync(dl, &tr->lim[b], n * 2, hipMemcpyHostToDevice, s));
         const int rc = rl_router_step(r, n, dk, dp, dt, dl, da, dr, s);
         if (rc != RL_OK && out->step_rc == RL_OK) out->step_rc = rc;
+        // nosync_finish: the last step's work is still queued on s when finish is called
+        // (finish must wait for it itself)
+        if (nosync_finish && st == steps - 1) out->finish = rl_router_finish(r);
         HIPC(hipMemcpyAsync(&out->a[(size_t)st * n], da, n, hipMemcpyDeviceToHost, s));
         HIPC(hipMemcpyAsync(&out->r[(size_t)st * n], dr, n * 8, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
     }
-    out->finish = rl_router_finish(r);
+    if (!nosync_finish) out->finish = rl_router_finish(r);
     rl_router_destroy(r);
     HIPC(hipFree(dk)); HIPC(hipFree(dp)); HIPC(hipFree(dt)); HIPC(hipFree(dl)); HIPC(hipFree(da)); HIPC(hipFree(dr));
     HIPC(hipStreamDestroy(s));
@@ -208,7 +212,7 @@ static void loop_case(int G, size_t n, int steps, int64_t span_ms, bool regress,
     std::vector<Result> res(G);
     std::vector<std::thread> th;
     for (int rank = 0; rank < G; ++rank)
-        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, dir, (uint64_t)1 << 16, &res[rank], nullptr);
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, dir, (uint64_t)1 << 16, &res[rank], nullptr, false);
     for (auto& x : th) x.join();
     for (int rank = 0; rank < G; ++rank) {
         CHECK(res[rank].step_rc == RL_OK);
@@ -216,6 +220,53 @@ static void loop_case(int G, size_t n, int steps, int64_t span_ms, bool regress,
         if (dir) CHECK(res[rank].placed == 16 && res[rank].placed == res[0].placed);
     }
     compare(tr, G, n, steps, res, what);
+}
+
+// finish called right after the last step, with that step still queued on the caller's
+// stream (finish must order itself after it)
+static void loop_nosync_finish_case() {
+    const int G = 2;
+    const size_t n = 60000;
+    const int steps = 2;
+    Trace tr = make_trace((size_t)G * n * steps, 0xF1515, 30000, true);
+    Loop loop(G);
+    std::vector<Result> res(G);
+    std::vector<std::thread> th;
+    for (int rank = 0; rank < G; ++rank)
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1 << 16, &res[rank],
+                        nullptr, true);
+    for (auto& x : th) x.join();
+    for (int rank = 0; rank < G; ++rank) CHECK(res[rank].step_rc == RL_OK && res[rank].finish == RL_OK);
+    compare(tr, G, n, steps, res, "G=2 finish without a caller sync");
+}
+
+// Sources whose first requests lie within 2^30 ms of each other, one of them spanning far
+// past the other's compact window: the merged batch must run in full width (the router
+// decides from the sources' real now ranges), not be rejected as a span overflow.
+static void loop_span_case() {
+    const int G = 2;
+    const size_t n = 4000;
+    Trace tr;
+    const int64_t NS = 1000000, T0 = 1700000000000LL;
+    for (size_t i = 0; i < (size_t)G * n; ++i) {
+        const size_t rank = i / n, j = i % n;
+        int64_t ms;
+        if (rank == 0) ms = T0 + (int64_t)j;
+        else ms = T0 + ((int64_t)1 << 30) - 1000 + (int64_t)j * (((int64_t)1 << 31) / (int64_t)n);
+        tr.key.push_back(mix(i * 7919 + 3));                   // distinct keys
+        tr.permits.push_back(1 + (int32_t)(mix(i) % 3));
+        tr.now.push_back(ms * NS);
+        tr.lim.push_back((uint16_t)(i % 2));
+    }
+    Loop loop(G);
+    std::vector<Result> res(G);
+    std::vector<std::thread> th;
+    for (int rank = 0; rank < G; ++rank)
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, 1, false, (uint64_t)1 << 14, &res[rank],
+                        nullptr, false);
+    for (auto& x : th) x.join();
+    for (int rank = 0; rank < G; ++rank) CHECK(res[rank].step_rc == RL_OK && res[rank].finish == RL_OK);
+    compare(tr, G, n, 1, res, "G=2 merged span > 2^31 ms (bases within 2^30)");
 }
 
 static void loop_error_case() {
@@ -230,7 +281,7 @@ static void loop_error_case() {
     std::vector<Result> res(G);
     std::vector<std::thread> th;
     for (int rank = 0; rank < G; ++rank)
-        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1, &res[rank], nullptr);
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1, &res[rank], nullptr, false);
     for (auto& x : th) x.join();
     for (int rank = 0; rank < G; ++rank) {
         const bool failed = res[rank].step_rc == RL_E_CAPACITY || res[rank].finish == RL_E_CAPACITY;
@@ -249,6 +300,8 @@ int main(int argc, char** argv) {
         loop_case(2, 50000, 2, (int64_t)1 << 36, false, false, "G=2 wide (span > 2^32 ms)");
         loop_case(4, 50000, 3, 30000, true, false, "G=4 TB regression (exception blocks)");
         loop_case(4, 50000, 3, 30000, false, true, "G=4 hot-key directory");
+        loop_nosync_finish_case();
+        loop_span_case();
         loop_error_case();
     } else if (mode == "rccl") {
         char id[RL_RCCL_ID_BYTES];

@@ -51,11 +51,15 @@ def synth(eng, cfg, t0_ns, n, index_base=0, steps=13):
     return keys, permits, now, lim
 
 
-def run_config(name, n, batches, pipeline=False, cuts=None):
+def run_config(name, n, batches, pipeline=False, cuts=None, cfg=None, tune=()):
     """`pipeline`: RL_OPT_PIPELINE, every batch submitted back-to-back with no sync in between
-    (batch b+1's partition overlaps batch b's decisions); `cuts`: explicit batch boundaries."""
+    (batch b+1's partition overlaps batch b's decisions); `cuts`: explicit batch boundaries;
+    `cfg`: a workload of bench.CONFIGS' shape not in it. Token-bucket balances
+    (tokens_after) are compared bit-for-bit with the oracle's (Lua reply,
+    TokenBucketRateLimiter.java:56-67; north_star asks 1e-9 relative)."""
     cfgs, t0_ns = bench_configs()
-    cfg = cfgs[name]
+    cfg = cfg or cfgs[name]
+    has_tb = any(l[0] == rl_amd.TB for l in cfg["limiters"])
     if cuts is None:
         per = (n + batches - 1) // batches
         cuts = [min(n, b * per) for b in range(batches + 1)]
@@ -63,15 +67,18 @@ def run_config(name, n, batches, pipeline=False, cuts=None):
     eng = rl_amd.Engine(device=0, max_batch=per, capacity=cfg["capacity"], pipeline=pipeline)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)
+    for k, v in tune:
+        eng.tune(k, v)
     keys, permits, now, lim = synth(eng, cfg, t0_ns, n)
     allowed = torch.empty(n, dtype=torch.uint8, device="cuda")
     remaining = torch.empty(n, dtype=torch.int64, device="cuda")
+    tokens = torch.empty(n, dtype=torch.float64, device="cuda") if has_tb else None
     torch.cuda.synchronize()                    # inputs complete before the (pipelined) calls
     for a, b in zip(cuts, cuts[1:]):
         sl = slice(a, b)
         m = sl.stop - sl.start
         eng.execute_device(m, keys[sl], permits[sl], now[sl], None if lim is None else lim[sl],
-                           None, allowed[sl], remaining[sl])
+                           None, allowed[sl], remaining[sl], None if tokens is None else tokens[sl])
         if not pipeline:
             assert eng.last_status() == rl_amd.RL_OK, rl_amd.strerror(eng.last_status())
     eng.sync()
@@ -81,11 +88,15 @@ def run_config(name, n, batches, pipeline=False, cuts=None):
     p = permits.cpu().numpy()
     t = now.cpu().numpy()
     li = None if lim is None else lim.cpu().numpy().view(np.uint16)
-    got = (allowed.cpu().numpy(), remaining.cpu().numpy(), None)
-    del keys, permits, now, lim, allowed, remaining
+    got = (allowed.cpu().numpy(), remaining.cpu().numpy(),
+           None if tokens is None else tokens.cpu().numpy())
+    del keys, permits, now, lim, allowed, remaining, tokens
     eng.close()
     o = COracle(cfg["limiters"], nthreads=ORACLE_THREADS)
-    want = o.run(k, p, t, li, None, want_tokens=False)
+    want = o.run(k, p, t, li, None, want_tokens=has_tb)
+    if has_tb:
+        assert got[2] is not None and want[2] is not None
+        assert np.isfinite(want[2]).sum() > 0          # balances really compared
     o.close()
     assert_same(got, want, name)
     return k, got, st
@@ -115,6 +126,41 @@ def test_config_mixed_tenants_pipelined_ragged():
 
 def test_config_zipf_1b_16m():
     k, got, _ = run_config("zipf_1b", 1 << 24, 2)
+    assert 0 < got[0].sum() < len(k)
+
+
+def test_config_tb_uniform_one_batch_balances():
+    """configs[1] exactly as bench.py's step 0: one whole 64M-request batch, balances and all."""
+    cfgs, _ = bench_configs()
+    n = cfgs["tb_uniform"]["batch"]
+    k, got, _ = run_config("tb_uniform", n, 1)
+    assert 0 < got[0].sum() < len(k)
+    assert np.isfinite(got[2]).all()
+
+
+def test_tb_hot_keys_at_limit():
+    """Token-bucket hot keys at their limit through the hot chains (k_hot_chains, default
+    hot_threshold): TB 50 at 10/s, Zipf s=1.1 over 1M keys, 8M requests over 4 s in 2
+    batches — the top key draws ~1M requests, hundreds of regions go hot, and the chains'
+    "denied by time alone" blocks and [T0, T1) runs are checked balance by balance
+    (Lua TokenBucketRateLimiter.java:46-67)."""
+    cfg = dict(limiters=[(rl_amd.TB, 50, 60_000, 10.0)], n_keys=1_000_000, dist=rl_amd.DIST_ZIPF,
+               zipf_s=1.1, batch=1 << 22, span_ns=2_000 * 1_000_000,
+               permits_max=3, seed=0x5EED00B1, capacity=1 << 20)
+    k, got, st = run_config("tb_hot", 1 << 23, 2, cfg=cfg)
+    _, c = np.unique(k, return_counts=True)
+    assert c.max() > 16384 * 4                   # several hot regions per batch
+    a = got[0]
+    assert 0 < a.sum() < len(k)
+
+
+def test_tb_hot_keys_forced_chains():
+    """Every region with >= 64 records through the hot path (hot_threshold 64): mixed
+    time-regressing-free TB traffic where most regions run the chains, balances bit-exact."""
+    cfg = dict(limiters=[(rl_amd.TB, 50, 60_000, 10.0), (rl_amd.TB, 1000, 60_000, 100.0)],
+               n_keys=200_000, dist=rl_amd.DIST_ZIPF, zipf_s=1.1, batch=1 << 21,
+               span_ns=4_000 * 1_000_000, permits_max=4, seed=0x5EED00B2, capacity=1 << 18)
+    k, got, _ = run_config("tb_forced", 1 << 22, 2, cfg=cfg, tune=(("hot_threshold", 64),))
     assert 0 < got[0].sum() < len(k)
 
 

@@ -138,9 +138,11 @@ def test_wire_pack_unwire_roundtrip():
     assert hdr.cpu().tolist()[1] == 1
 
 
-def _bench_worker(rank, world, port, cfg_name, steps, n, out):
+def _bench_worker(rank, world, port, cfg_name, steps, n, out, kind="python"):
     """One rank of bench.py's N-GPU path on the shared GPU: its slice of the exact bench
-    trace (k_synth, same seed / key population / time axis as `bench.py --gpus world`)."""
+    trace (k_synth, same seed / key population / time axis as `bench.py --gpus world`).
+    kind "capi": the C-ABI router (rl_router_*, what bench.py --gpus N drives) over the host
+    transport, with the hot-key directory planned from the first slice as bench.py does."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
@@ -155,18 +157,38 @@ def _bench_worker(rank, world, port, cfg_name, steps, n, out):
                         shard_count=world)
     for l in cfg["limiters"]:
         eng.add_limiter(*l)
-    router = Router(DeviceOps(eng, world, dev, n), world, rank, exchange_device="cpu")
+    slices = []
+    for s in range(steps):
+        slices.append(_bench_slice(eng, cfg, s, rank, world, steps, n))
+    eng.sync()                                      # k_synth ran on the engine stream
+    placed = 0
+    if kind == "capi":
+        from rl_amd.capi_router import CRouter
+        router = CRouter(eng, world, rank, n, transport="host", device=0)
+        if cfg["dist"] == rl_amd.DIST_ZIPF:
+            placed = bench.plan_directory(router, cfg, slices, n, k=1024, sample=1 << 20)
+            assert placed == 1024
+
+        def step(k, p, t, a, r, li):
+            router.step(n, k, p, t, li, a, r)
+            torch.cuda.synchronize()
+    else:
+        router = Router(DeviceOps(eng, world, dev, n), world, rank, exchange_device="cpu")
+
+        def step(k, p, t, a, r, li):
+            router.step(k, p, t, a, r, li)
+            eng.sync()
     res_a, res_r = [], []
     for s in range(steps):
-        k, p, t, li = _bench_slice(eng, cfg, s, rank, world, steps, n)
-        eng.sync()                                  # k_synth ran on the engine stream
+        k, p, t, li = slices[s]
         a = torch.empty(n, dtype=torch.uint8, device=dev)
         r = torch.empty(n, dtype=torch.int64, device=dev)
-        router.step(k, p, t, a, r, li)
-        eng.sync()
+        step(k, p, t, a, r, li)
         res_a.append(a.cpu().numpy())
         res_r.append(r.cpu().numpy())
     assert router.finish() == rl_amd.RL_OK
+    if kind == "capi":
+        router.close()
     np.savez(f"{out}.{rank}.npz", a=np.concatenate(res_a), r=np.concatenate(res_r))
     dist.destroy_process_group()
 
@@ -187,10 +209,12 @@ def _bench_slice(eng, cfg, s, rank, world, steps, n):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("kind", ["python", "capi"])
 @pytest.mark.parametrize("cfg_name", ["mixed_tenants", "zipf_1b"])
-def test_two_shards_bench_configs(tmp_path, cfg_name):
+def test_two_shards_bench_configs(tmp_path, cfg_name, kind):
     """BASELINE configs[3] / [4] (bench.py's 10-limiter and TB + SW Zipf workloads) through
-    the 2-shard router, 2M requests per rank per step, against the oracle on the global stream."""
+    the 2-shard router, 2M requests per rank per step, against the oracle on the global stream;
+    both the torch.distributed router and the C-ABI one (with its hot-key directory)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
@@ -202,7 +226,7 @@ def test_two_shards_bench_configs(tmp_path, cfg_name):
     s.close()
     world, steps, n = 2, 2, 1 << 21
     out = str(tmp_path / "b")
-    mp.spawn(_bench_worker, args=(world, port, cfg_name, steps, n, out), nprocs=world, join=True)
+    mp.spawn(_bench_worker, args=(world, port, cfg_name, steps, n, out, kind), nprocs=world, join=True)
     cfg = bench.CONFIGS[cfg_name]
     torch.cuda.set_device(0)
     gen = rl_amd.Engine(device=0, max_batch=n, capacity=1 << 10)
