@@ -2,7 +2,7 @@
 //
 // Owns, per GPU: the HBM state table (one region array per limiter), the
 // limiter table, the batch scratch and one HIP stream. A batch is a fixed chain
-// of kernel launches on that stream (see rl_kernels.hip); nothing in the chain
+// of kernel launches on that stream (see csrc/rl_*.hip); nothing in the chain
 // synchronises with the host, so the device entry point is fully asynchronous.
 #include <hip/hip_runtime.h>
 

@@ -1,4 +1,4 @@
-// rl_launch.hpp — host-side launchers for the kernels in rl_kernels.hip.
+// rl_launch.hpp — host-side launchers for the kernels in csrc/rl_*.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -247,6 +247,15 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
 // without it the chains share the normal regions' launch (2-wave workgroups).
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
                          hipStream_t hs = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+// the hot chains' side-stream launch, and the one-launch variant (split_hot 0)
+hipError_t launch_hot_chains(const RegionArgs& a, bool wide, int res_bytes, hipStream_t hs);
+hipError_t launch_regions_combined(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
+// per record codec / packed result width (instantiated in csrc/rl_rt_*.hip)
+template <class Codec, class Res>
+hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0, hipEvent_t e1);
+template <class Codec, class Res> hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs);
+template <class Codec, class Res> hipError_t regions_combined_t(const RegionArgs& a, hipStream_t s);
+template <class Codec, class Res> hipError_t hot_fill_t(const RegionArgs& a, hipStream_t s);
 hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s);
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s);   // prep, scan, summaries
 hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);

@@ -1,0 +1,560 @@
+// rl_partition.hip — stable partition of a batch into region order (upsweep, scans,
+// scatter, bin bounds) and the unpermute back to arrival order, for gfx950.
+#include "rl_kcommon.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rl {
+
+// ------------------------------------------------------------------ 1. upsweep
+template <class Codec, bool RAW>
+__global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
+    __shared__ uint32_t hist[1u << kMaxDigitBits];
+    __shared__ LimLds L;
+    const uint32_t t = threadIdx.x;
+    const uint32_t bins = 1u << a.digit_bits;
+    load_lim_lds(L, a);
+    if constexpr (RAW) {
+        if (blockIdx.x == 0 && t == 0) {
+            BatchCtl* c = a.ctl;
+            c->base_ms = floor_div_ms(a.now_ns[0]) - (1LL << 31);
+            c->min_now_key = ~0ULL;
+            c->max_now_key = 0;
+            c->span_overflow = 0;
+            c->n_esc = 0;
+            c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = c->cache_hits = 0;
+            c->grow[0] = c->grow[1] = c->grow[2] = c->grow[3] = 0;
+            c->table_bytes = 0;
+        }
+    }
+    const uint32_t mask = bins - 1;
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t tile = tile_at(it, a.n_tiles);
+        if (tile >= a.n_tiles) break;
+        for (uint32_t b = t; b < bins; b += kTileThreads) hist[b] = 0;
+        __syncthreads();
+#pragma unroll 8
+        for (int r = 0; r < kTileItems; ++r) {
+            const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+            if (i < a.n) {
+                const uint32_t g = bin_of<Codec, RAW>(a, i, L);
+                atomicAdd(&hist[(g >> a.digit_shift) & mask], 1u);
+                if (a.region_count) atomicAdd(&a.region_count[g], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t b = t; b < bins; b += kTileThreads)
+            a.counts[(size_t)b * a.n_tiles + tile] = hist[b];
+    }
+}
+
+// ------------------------------------------------------------------ 2. scans
+// Exclusive scan of each row of a [rows][cols] matrix (one block per row).
+__global__ __launch_bounds__(256) void k_scan_rows(const uint32_t* in, uint32_t* out,
+                                                   uint32_t cols, uint32_t* totals) {
+    __shared__ uint32_t tmp[4];
+    const size_t row = blockIdx.x;
+    const uint32_t* src = in + row * cols;
+    uint32_t* dst = out + row * cols;
+    const uint32_t chunk = (cols + 255) / 256;
+    const uint32_t beg = min(threadIdx.x * chunk, cols);
+    const uint32_t end = min(beg + chunk, cols);
+    uint32_t sum = 0;
+    for (uint32_t k = beg; k < end; ++k) sum += src[k];
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<256>(sum, tmp, &tot);
+    for (uint32_t k = beg; k < end; ++k) {
+        const uint32_t v = src[k];
+        dst[k] = run;
+        run += v;
+    }
+    if (threadIdx.x == 0) totals[row] = tot;
+}
+
+// Single-block exclusive scan of a short array (<= a few million entries).
+__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* in, uint32_t* out,
+                                                     uint32_t len) {
+    __shared__ uint32_t tmp[16];
+    const uint32_t chunk = (len + 1023) / 1024;
+    const uint32_t beg = min(threadIdx.x * chunk, len);
+    const uint32_t end = min(beg + chunk, len);
+    uint32_t sum = 0;
+    for (uint32_t k = beg; k < end; ++k) sum += in[k];
+    uint32_t run = block_exclusive_scan<1024>(sum, tmp, nullptr);
+    for (uint32_t k = beg; k < end; ++k) {
+        const uint32_t v = in[k];
+        out[k] = run;
+        run += v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_add_rows(const uint32_t* row_base, uint32_t* data,
+                                                  uint32_t cols) {
+    const size_t row = blockIdx.x;
+    const uint32_t b = row_base[row];
+    for (uint32_t k = threadIdx.x; k < cols; k += 256) data[row * cols + k] += b;
+}
+
+// ------------------------------------------------------------------ 3. scatter
+// Stable: a tile's elements are ranked in (round, wave, lane) order, which is the
+// arrival order; tiles are ordered by the exclusive [bin][tile] scan. The inputs of
+// round r+1 are loaded into registers before round r is ranked, so the global-load
+// latency hides behind the two LDS barriers of a round.
+template <class Codec, bool RAW>
+struct ScatterIn;
+
+template <class Codec>
+struct ScatterIn<Codec, true> {
+    uint64_t key; int64_t now_ns; int32_t permits; uint32_t lim; uint32_t op;
+    __device__ inline void load(const PartArgs& a, uint32_t i) {
+        key = ld<kNtScIn>(a.key + i);
+        now_ns = ld<kNtScIn>(a.now_ns + i);
+        permits = ld<kNtScIn>(a.permits + i);
+        lim = a.limiter ? a.limiter[i] : 0u;
+        op = a.op ? a.op[i] : 0u;
+    }
+};
+
+template <class Codec>
+struct ScatterIn<Codec, false> {
+    typename Codec::Rec rec;
+    __device__ inline void load(const PartArgs& a, uint32_t i) {
+        rec = ((const typename Codec::Rec*)a.rec_in)[i];
+    }
+};
+
+#ifndef RL_SCATTER_DEPTH
+#define RL_SCATTER_DEPTH 8
+#endif
+constexpr int kScatterDepth = RL_SCATTER_DEPTH;   // rounds of inputs in flight (divides kTileItems)
+
+template <class Codec, bool RAW>
+__global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
+    using Rec = typename Codec::Rec;
+    static_assert(kTileThreads / 64 <= 8, "per-wave counts are packed 8 to a bin");
+    __shared__ uint32_t cur[1u << kMaxDigitBits];                    // next slot per bin
+    // this round's count of each wave per bin, the waves' bytes packed in one word: a lane
+    // sums the earlier waves' counts for its bin with one read and two v_sad_u8
+    __shared__ uint64_t cntw[1u << kMaxDigitBits];
+    __shared__ LimLds L;
+    __shared__ uint64_t s_mm[2][kTileThreads / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t bins = 1u << a.digit_bits, mask = bins - 1;
+    load_lim_lds(L, a);
+    int64_t base = 0;
+    if constexpr (RAW) base = a.ctl->base_ms;
+    const uint32_t last = a.n - 1;
+    uint64_t mn = ~0ULL, mx = 0;
+    bool overflow = false;
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t tile = tile_at(it, a.n_tiles);
+        if (tile >= a.n_tiles) break;
+        const uint32_t tile0 = tile * (uint32_t)kTile;
+        __syncthreads();     // previous tile's LDS users are done
+        for (uint32_t b = t; b < bins; b += kTileThreads) {
+            cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
+            cntw[b] = 0;
+        }
+        // kScatterDepth rounds of inputs in flight; out-of-range lanes re-load element n-1
+        // so every wave issues the same loads and stores each round (static vmcnt counting)
+        ScatterIn<Codec, RAW> in[kScatterDepth];
+#pragma unroll
+        for (int k = 0; k < kScatterDepth; ++k) in[k].load(a, min(tile0 + (uint32_t)k * kTileThreads + t, last));
+        __syncthreads();
+        auto round = [&](const ScatterIn<Codec, RAW>& in, int r) {
+            const uint32_t i = tile0 + (uint32_t)r * kTileThreads + t;
+            const bool active = i < a.n;
+            Rec rec{};
+            uint32_t d = 0;
+            if (active) {
+                if constexpr (RAW) {
+                    uint32_t lim = in.lim, op = in.op;
+                    const int32_t p = in.permits;
+                    const int64_t now_ms = floor_div_ms(in.now_ns);
+                    const bool lim_ok = lim < a.n_lim;
+                    if (!lim_ok) lim = 0;
+                    const bool invalid = !lim_ok || op > 2u || (op == 0u && p <= 0);
+                    if (op > 2u) op = 0;
+                    const uint64_t h = mix64(in.key);
+                    rec = Codec::enc(h, now_ms, base, p, op, lim, invalid);
+                    // an invalid request's now is never read: it neither widens the batch's
+                    // time range nor rejects the batch for its span
+                    if (!invalid) {
+                        const int64_t rel = now_ms - base;
+                        // only the compact record keeps now relative to base
+                        if constexpr (std::is_same<Codec, CodecC>::value)
+                            overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
+                        const uint64_t k = ord_key(now_ms);
+                        mn = k < mn ? k : mn;
+                        mx = k > mx ? k : mx;
+                    }
+                    d = (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                         >> a.digit_shift) & mask;
+                } else {
+                    rec = in.rec;
+                    const uint32_t lim = Codec::limiter_of(rec);
+                    d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                         >> a.digit_shift) & mask;
+                }
+            }
+            const uint32_t abl = a.ablate;
+            const uint64_t m = (abl & kAblNoMatch) ? (1ULL << lane) : wave_match(d, a.digit_bits, active);
+            const uint32_t lr = popc_below(m);
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            const bool leader = active && lr == 0;
+            if (leader) ((uint8_t*)&cntw[d])[wid] = (uint8_t)cnt;
+            if (!(abl & kAblNoBarrier)) __syncthreads();
+            uint32_t pos = 0;
+            if (active) {
+                const uint64_t below = wid == 0 ? 0ULL : cntw[d] & ((1ULL << (8 * wid)) - 1);
+                pos = cur[d] + lr + __builtin_amdgcn_sad_u8((uint32_t)below, 0u, 0u) +
+                      __builtin_amdgcn_sad_u8((uint32_t)(below >> 32), 0u, 0u);
+            }
+            if (!(abl & kAblNoBarrier)) __syncthreads();
+            if (leader) {
+                atomicAdd(&cur[d], cnt);
+                ((uint8_t*)&cntw[d])[wid] = 0;
+            }
+            if (abl & (kAblNoMatch | kAblNoBarrier)) pos = min(pos, a.n - 1);
+            // inactive lanes write to the padding slot past n (buffers carry spare entries)
+            uint32_t wpos = active ? pos : a.n + t;
+            if (abl & kAblSeqRecStore) wpos = active ? i : a.n + t;
+            if (!(abl & kAblNoRecStore)) st_rec<kNtScRec>((Rec*)a.rec_out + wpos, rec);
+            if (!(abl & kAblNoPosStore)) st<kNtScPos>(a.pos_out + (active ? i : a.n + t), pos);
+        };
+        // Unrolled by the prefetch depth so the input registers rotate without moves (a
+        // move would wait on its load). vmcnt retires loads and stores in issue order, so
+        // waiting for round r's inputs also waits for the scattered stores issued before
+        // them: a deep ring spreads that store-ack latency over kScatterDepth rounds.
+        for (int r = 0; r < kTileItems; r += kScatterDepth) {
+#pragma unroll
+            for (int k = 0; k < kScatterDepth; ++k) {
+                round(in[k], r + k);
+                in[k].load(a, min(tile0 + (uint32_t)(r + k + kScatterDepth) * kTileThreads + t, last));
+            }
+        }
+    }
+    if constexpr (RAW) {
+        // min / max now over this workgroup's tiles -> one atomic each
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a1 = __shfl_xor(mn, o, 64), b1 = __shfl_xor(mx, o, 64);
+            mn = a1 < mn ? a1 : mn;
+            mx = b1 > mx ? b1 : mx;
+        }
+        __syncthreads();
+        if (lane == 0) { s_mm[0][wid] = mn; s_mm[1][wid] = mx; }
+        const bool any_over = __syncthreads_or(overflow);
+        if (t == 0) {
+            for (int w = 1; w < kTileThreads / 64; ++w) {
+                mn = s_mm[0][w] < mn ? s_mm[0][w] : mn;
+                mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
+            }
+            if (mn != ~0ULL) atomicMin((unsigned long long*)&a.ctl->min_now_key, (unsigned long long)mn);
+            if (mx != 0) atomicMax((unsigned long long*)&a.ctl->max_now_key, (unsigned long long)mx);
+            if (any_over) atomicOr(&a.ctl->span_overflow, 1u);
+        }
+    }
+}
+
+// Bin boundaries of the final record order (two-pass partitions): rstart[b] / rend[b]
+// for every bin b < n_bins. The high-digit pass leaves run hi = [hi_base[hi],
+// hi_base[hi] + hi_total[hi]) whose records are still in low-digit order (the pass is
+// stable over the low-digit pass's output), so each low digit's first record is a
+// binary search inside its run: one workgroup per run, ~log2(run) record probes per
+// bin instead of reading every record of the batch.
+template <class Codec>
+__global__ __launch_bounds__(256) void k_bin_bounds(BoundsArgs a) {
+    __shared__ uint32_t s_base[256];
+    __shared__ uint8_t s_bits[256];
+    __shared__ uint32_t s_lb[(1u << kMaxDigitBits) + 1];
+    for (uint32_t l = threadIdx.x; l < a.n_lim; l += 256) {
+        s_base[l] = a.lims[l].region_base;
+        s_bits[l] = (uint8_t)a.lims[l].region_bits;
+    }
+    __syncthreads();
+    const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
+    const uint32_t nlo = 1u << a.d0, lo_mask = nlo - 1;
+    auto lo_of = [&](uint32_t i) {
+        const typename Codec::Rec r = recs[i];
+        const uint32_t lim = Codec::limiter_of(r);
+        return ((s_base[lim] + region_local(r.h, a.shard_bits, s_bits[lim])) >> a.bin_shift) & lo_mask;
+    };
+    const uint32_t hi = blockIdx.x;
+    const uint32_t beg = a.hi_base[hi], end = beg + a.hi_total[hi];
+    for (uint32_t lo = threadIdx.x; lo <= nlo; lo += 256) {
+        uint32_t L = beg, R = end;                    // first record with low digit >= lo
+        if (lo == nlo) L = end;
+        while (L < R) {
+            const uint32_t m = L + (R - L) / 2;
+            if (lo_of(m) < lo) L = m + 1;
+            else R = m;
+        }
+        s_lb[lo] = L;
+    }
+    __syncthreads();
+    for (uint32_t lo = threadIdx.x; lo < nlo; lo += 256) {
+        const uint32_t b = (hi << a.d0) | lo;
+        if (b < a.n_bins) {
+            a.rstart[b] = s_lb[lo];
+            a.rend[b] = s_lb[lo + 1];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 5. unpermute
+template <class Res>
+__global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
+  const uint32_t t = threadIdx.x;
+  const Res* __restrict__ res = (const Res*)a.res;
+  const uint32_t* __restrict__ pos0 = a.pos0;
+  const uint32_t* __restrict__ pos1 = a.pos1;
+  uint8_t* __restrict__ allowed = a.allowed;
+  int64_t* __restrict__ remaining = a.remaining;
+  constexpr int B = 8;                         // rounds per batch (loads issued together)
+  constexpr int NB = kTileItems / B;
+  const bool simple = pos1 || a.tokens_out || (a.ablate & kAblNoGather);
+  for (uint32_t it = 0;; ++it) {
+    const uint32_t tile = tile_at(it, a.n_tiles);
+    if (tile >= a.n_tiles) break;
+    const uint32_t tbase = tile * (uint32_t)kTile + t;
+    if (!simple && tile * (uint64_t)kTile + kTile <= a.n) {
+        // Full tile, one result array: software-pipelined so that every wait is for loads
+        // issued a batch earlier and never directly behind the previous batch's stores
+        // (vmcnt retires loads and stores in issue order).
+        uint32_t pE[B], pO[B];
+        Res vE[B], vO[B];
+        auto load = [&](uint32_t (&p)[B], int b) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) p[k] = ld<kNtUn>(pos0 + tbase + (uint32_t)(b * B + k) * kTileThreads);
+        };
+        auto gather = [&](Res (&v)[B], const uint32_t (&p)[B]) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+        };
+        auto store = [&](const Res (&v)[B], int b) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) {
+                const uint32_t i = tbase + (uint32_t)(b * B + k) * kTileThreads;
+                st<kNtUn>(allowed + i, (uint8_t)(v[k] & 1u));
+                st<kNtUn>(remaining + i, (int64_t)(v[k] >> 1) - kResBias);
+            }
+        };
+        load(pE, 0);
+        for (int b = 0; b < NB; b += 2) {
+            gather(vE, pE);
+            load(pO, b + 1);
+            if (b > 0) store(vO, b - 1);
+            gather(vO, pO);
+            load(pE, (b + 2) % NB);                 // unconditional (last one unused)
+            store(vE, b);
+        }
+        store(vO, NB - 1);
+        continue;
+    }
+    for (int r0 = 0; r0 < kTileItems; r0 += B) {
+        uint32_t p[B];
+        Res v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const uint32_t i = tile * (uint32_t)kTile + (uint32_t)(r0 + k) * kTileThreads + t;
+            p[k] = pos0[i < a.n ? i : 0];
+        }
+        if (pos1) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) p[k] = pos1[p[k]];
+        }
+        if (a.ablate & kAblNoGather) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) v[k] = (Res)p[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const uint32_t i = tile * (uint32_t)kTile + (uint32_t)(r0 + k) * kTileThreads + t;
+            if (i < a.n) {
+                allowed[i] = (uint8_t)(v[k] & 1u);
+                remaining[i] = (int64_t)(v[k] >> 1) - kResBias;
+                if (a.tokens_out) a.tokens_out[i] = a.tok ? a.tok[p[k]] : __builtin_nan("");
+            }
+        }
+    }
+  }
+  if (a.ctl && a.ctl->n_esc != 0) {
+    // Rare (TB balances below -3 after time regression): the gather above decoded the
+    // escape code as (allowed 1, remaining -3); rewrite those results from the side array.
+    // Same tiles, same thread per element as above, so the rewrite follows the first store.
+    const Res* rf = (const Res*)a.res_final;
+    for (uint32_t it = 0;; ++it) {
+      const uint32_t tile = tile_at(it, a.n_tiles);
+      if (tile >= a.n_tiles) break;
+      for (int r = 0; r < kTileItems; ++r) {
+        const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+        if (i >= a.n) break;
+        uint32_t j = pos0[i];
+        if (a.pos1_final) j = a.pos1_final[j];
+        if ((uint64_t)rf[j] == kResEscape) {
+          allowed[i] = 0;
+          remaining[i] = a.ext[j];
+        }
+      }
+    }
+  }
+}
+
+// Two-pass batches: undo the high-digit pass first. mid[j] = res[pos1[j]] for j in
+// pass-0 order: pos1 is read in order and, since pass 0 left the records sorted by low
+// digit, consecutive j fall into one low-digit run whose elements go to the 2^d1
+// high-digit bins in order — the gather walks 2^d1 sequential streams instead of the
+// whole result array. k_unpermute then gathers mid[pos0[i]] (2^d0 streams). Two
+// local gathers replace the composed res[pos1[pos0[i]]], which hit a random line of a
+// 1 GB index and of the result array per request.
+template <class Res>
+__global__ __launch_bounds__(256) void k_unpermute_mid(const uint32_t* __restrict__ pos1,
+                                                       const Res* __restrict__ res,
+                                                       Res* __restrict__ mid, uint32_t n) {
+    constexpr int B = 8;
+    const uint32_t base = blockIdx.x * (256u * B) + threadIdx.x;
+    uint32_t p[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const uint32_t j = base + (uint32_t)k * 256u;
+        p[k] = pos1[j < n ? j : 0];
+    }
+    Res v[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        const uint32_t j = base + (uint32_t)k * 256u;
+        if (j < n) mid[j] = v[k];
+    }
+}
+
+__global__ void k_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        allowed[i] = 0;
+        remaining[i] = kRemInvalid;
+        if (tok) tok[i] = __builtin_nan("");
+    }
+}
+
+
+hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
+    dim3 grid(persistent_grid(a.n_tiles, a.up_per_cu ? a.up_per_cu : 4)), block(kTileThreads);
+    if (raw) {
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, true>), grid, block, 0, s, a);
+    } else {
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
+    dim3 grid(persistent_grid(a.n_tiles, a.sc_per_cu ? a.sc_per_cu : 1)), block(kTileThreads);
+    if (raw) {
+        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, 0, s, a);
+    } else {
+        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_scatter<CodecC, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, uint32_t cols,
+                            uint32_t* totals, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_rows, dim3(rows), dim3(256), 0, s, in, out, cols, totals);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, in, out, len);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
+                           uint32_t cols, hipStream_t s) {
+    hipLaunchKernelGGL(k_add_rows, dim3(rows), dim3(256), 0, s, row_base, data, cols);
+    return hipGetLastError();
+}
+
+// Fold the sharded batch counters into BatchCtl and clear them for the next batch.
+__global__ __launch_bounds__(256) void k_stats_reduce(unsigned long long* stats, BatchCtl* ctl) {
+    __shared__ unsigned long long part[kStWords][4];
+    const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    unsigned long long acc[kStCount] = {};
+    for (uint32_t s = t; s < kStatSlots; s += 256) {
+        unsigned long long* p = stats + (size_t)s * kStWords;
+#pragma unroll
+        for (int k = 0; k < (int)kStCount; ++k) { acc[k] += p[k]; p[k] = 0; }
+    }
+#pragma unroll
+    for (int k = 0; k < (int)kStCount; ++k) {
+        unsigned long long v = acc[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) part[k][wid] = v;
+    }
+    __syncthreads();
+    if (t < kStCount) {
+        const unsigned long long v = part[t][0] + part[t][1] + part[t][2] + part[t][3];
+        unsigned long long* dst = t == kStAllowed ? &ctl->allowed : t == kStInvalid ? &ctl->invalid
+                                : t == kStCapErr ? &ctl->cap_err : t == kStDistinct ? &ctl->distinct
+                                : t == kStRegions ? &ctl->regions : t == kStCacheHits ? &ctl->cache_hits
+                                : &ctl->table_bytes;
+        *dst += v;
+    }
+}
+
+hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats, ctl);
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s) {
+    if (a.n_bins == 0 || a.d0 > kMaxDigitBits || a.d1 > kMaxDigitBits || a.d0 < 1)
+        return hipErrorInvalidValue;
+    const dim3 g(1u << a.d1), b(256);
+    if (wide) hipLaunchKernelGGL(k_bin_bounds<CodecW>, g, b, 0, s, a);
+    else hipLaunchKernelGGL(k_bin_bounds<CodecC>, g, b, 0, s, a);
+    return hipGetLastError();
+}
+
+template <class Res>
+static void unpermute_mid(const UnpermArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_unpermute_mid<Res>, dim3((a.n + 2047) / 2048), dim3(256), 0, s, a.pos1,
+                       (const Res*)a.res, (Res*)a.mid, a.n);
+}
+
+hipError_t launch_unpermute(const UnpermArgs& a_in, int res_bytes, hipStream_t s) {
+    UnpermArgs a = a_in;
+    a.res_final = a.res;
+    a.pos1_final = a.pos1;
+    if (a.pos1 && a.mid && !a.tokens_out && a.n) {      // two-pass: undo pass 1, then pass 0
+        if (res_bytes == 8) unpermute_mid<uint64_t>(a, s);
+        else if (res_bytes == 1) unpermute_mid<uint8_t>(a, s);
+        else if (res_bytes == 2) unpermute_mid<uint16_t>(a, s);
+        else unpermute_mid<uint32_t>(a, s);
+        a.res = a.mid;
+        a.pos1 = nullptr;
+    }
+    dim3 g(persistent_grid(a.n_tiles, a.per_cu ? a.per_cu : 1)), b(kTileThreads);
+    if (res_bytes == 8) hipLaunchKernelGGL(k_unpermute<uint64_t>, g, b, 0, s, a);
+    else if (res_bytes == 1) hipLaunchKernelGGL(k_unpermute<uint8_t>, g, b, 0, s, a);
+    else if (res_bytes == 2) hipLaunchKernelGGL(k_unpermute<uint16_t>, g, b, 0, s, a);
+    else hipLaunchKernelGGL(k_unpermute<uint32_t>, g, b, 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_fill_invalid, dim3((n + 255) / 256), dim3(256), 0, s, allowed,
+                       remaining, tok, n);
+    return hipGetLastError();
+}
+
+}  // namespace rl

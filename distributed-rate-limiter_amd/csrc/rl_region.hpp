@@ -1,0 +1,658 @@
+// rl_region.hpp — the per-region sequential semantics (wave_apply, region_body_t), shared by
+// the normal-region kernels (rl_region.hip) and the hot chains (rl_hot.hip).
+#pragma once
+#include "rl_kcommon.hpp"
+
+#pragma clang fp contract(off)
+
+namespace rl {
+
+// ------------------------------------------------------------------ 4. regions
+// One single-wave workgroup per REGION. The region's 256 slots (8 KB) live in the wave's
+// LDS for the whole batch. The wave streams its BIN's records (arrival order, 8
+// regions interleaved) 64 at a time, keeps the ones of its region in an LDS ring and
+// applies them 64 at a time. The 8 waves of a bin have block ids congruent mod 8 and
+// adjacent in dispatch order, i.e. they run together on one XCD, so the bin's stream is
+// fetched from HBM once and re-read from that XCD's L2. No barriers anywhere.
+
+
+struct RegionTable {
+    static constexpr bool kCache = false;
+    alignas(16) uint64_t tag[kRegionSlots];
+    uint64_t sa[kRegionSlots];
+    uint64_t sb[kRegionSlots];
+    uint64_t sc[kRegionSlots];
+    alignas(16) uint32_t occ[kRegionSlots];   // bit0 occupied, bit1 touched by this batch
+#ifdef RL_CHAINS
+    int64_t xrem[64];                         // wave_apply's per-key chains: results by lane
+    double xtok[64];
+    uint32_t xalw[64];
+#endif
+};
+// With a sliding-window local cache (SlidingWindowRateLimiter.java:57-64): every slot also
+// carries its key's cache state (block-until ms, sw_step_cache), moved with the slot.
+struct RegionTableX : RegionTable {
+    static constexpr bool kCache = true;
+    uint64_t sx[kRegionSlots];
+};
+
+template <class Codec, bool RING>
+struct RegionLds : RegionTable {
+    using Rec = typename Codec::Rec;
+    Rec ring[kRing];                  // this region's pending requests (bins of 8 regions)
+    uint32_t ring_pos[kRing];         // ... and their result index
+};
+template <class Codec>
+struct RegionLds<Codec, false> : RegionTable {};
+
+#ifndef RL_NO_SPARSE
+#define RL_NO_SPARSE 0                    // A/B builds: 1 compiles the sparse-region path out
+#endif
+constexpr bool kSparseOn = !RL_NO_SPARSE;
+
+// Sparse region (few records): the LDS table starts with every bucket kOccUnloaded and a
+// probe that reaches such a bucket faults it in from HBM (128 B, + 32 B of cache words);
+// dead slots come in as tombstones. tab == nullptr: the whole image is in LDS.
+struct SparseSrc {
+    const Slot* tab;
+    const uint64_t* xtab;             // local-cache words (nullable)
+    int64_t keep;                     // slot_live threshold (keep_from)
+    bool long_chain;                  // per lane: a probe went past two used buckets
+};
+
+template <class LdsT>
+__device__ inline void fault_bucket(const SparseSrc& sp, const DevLimiter& L, LdsT& S, uint32_t p) {
+    Slot v[4];
+    uint64_t x[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = sp.tab[p + k];
+    if constexpr (LdsT::kCache)
+        if (sp.xtab) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[k] = sp.xtab[p + k];
+        }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool fr = slot_free(v[k], x[k]);
+        const bool lv = !fr && slot_live(L, v[k], sp.keep, x[k]);
+        S.tag[p + k] = v[k].tag; S.sa[p + k] = v[k].a; S.sb[p + k] = v[k].b; S.sc[p + k] = v[k].c;
+        if constexpr (LdsT::kCache) S.sx[p + k] = x[k];
+        S.occ[p + k] = fr ? 0u : lv ? kOccUsed : (kOccUsed | kOccTomb);
+    }
+}
+
+struct Applied {
+    uint32_t j;                       // result index (padding slot for idle lanes)
+    bool alw;                         // allowed
+    int64_t rem;                      // remaining
+    double tok;
+};
+
+// Result store in partition order: packed in the width Res, or the escape code plus the
+// exact value in the int64 side array when remaining is outside Res's range (a TB
+// balance below -3 after time regression; see kResEscape).
+template <class Res>
+__device__ inline void put_res(const RegionArgs& a, uint32_t j, bool alw, int64_t rem) {
+    Res* res = (Res*)a.res;
+    if (res_fits<Res>(rem)) {
+        res[j] = (Res)pack_result(alw, rem);
+    } else {
+        res[j] = (Res)kResEscape;
+        a.ext[j] = rem;
+        atomicAdd(&a.ctl->n_esc, 1u);
+    }
+}
+
+// Growth signal of a region after its batch (lane 0): `used` live keys, or an overflow.
+__device__ inline void note_fill(const RegionArgs& a, uint32_t region, uint32_t used, bool overflow) {
+    if (used > kGrowUsed || overflow) {
+        const uint32_t li = a.region_lim[region];
+        atomicOr(&a.ctl->grow[li >> 6], 1ULL << (li & 63));
+    }
+}
+
+#ifdef RL_CHAINS
+// A/B build only (-DRL_CHAINS): measured slower than the rounds on every bench config
+// (same-box A/B: tb_uniform region 1.21 -> 1.28 ms, zipf_1b 6.16 -> 6.64, mixed 13.93 -> 14.03).
+// The per-key chains of wave_apply: every pending lane's key has its state in S[slot]; the
+// lowest pending lane of each key runs that key's pending requests in lane (= arrival) order,
+// reading each request's fields from its lane; results go through LDS back to their lanes.
+template <class Codec, int ALGO, class LdsT>
+__device__ inline void wave_chains(LdsT& S, const DevLimiter& L, uint32_t lane, const Req& q,
+                                   const SWGeo& geo, int32_t slot, bool& pending, uint64_t kp,
+                                   Applied& r, uint32_t& n_allowed) {
+    const bool leader = pending && (kp & ((1ULL << lane) - 1)) == 0;
+    uint64_t todo = leader ? kp : 0ULL;
+    uint64_t sa = 0, sb = 0, sc = 0;
+    if (leader) { sa = S.sa[slot]; sb = S.sb[slot]; sc = S.sc[slot]; }
+    while (__any(todo != 0)) {
+        const bool act = todo != 0;
+        const uint32_t l = act ? (uint32_t)__builtin_ctzll(todo) : lane;
+        todo &= todo - 1;
+        // every lane takes part in the shuffles (a source lane may be idle)
+        const int64_t t_l = __shfl(q.now_ms, (int)l, 64);
+        const int32_t p_l = __shfl(q.permits, (int)l, 64);
+        const uint32_t op_l = (uint32_t)__shfl((int)q.op, (int)l, 64);
+        Outcome o{};
+        if constexpr (ALGO == kAlgoTB) {
+            if (act) o = tb_step(L, op_l, p_l, t_l, sa, sb, sc);
+        } else {
+            SWGeo g;
+            g.curr_start = __shfl(geo.curr_start, (int)l, 64);
+            g.prev_start = __shfl(geo.prev_start, (int)l, 64);
+            g.prev_weight = __shfl(geo.prev_weight, (int)l, 64);
+            if (act) o = sw_step_g(L, op_l, p_l, t_l, g, sa, sb, sc);
+        }
+        if (act) {
+            S.xrem[l] = o.remaining;
+            S.xtok[l] = o.tokens;
+            S.xalw[l] = o.allowed ? 1u : 0u;
+            if (o.mutate) { sa = o.a; sb = o.b; sc = o.c; }
+        }
+    }
+    if (leader) { S.sa[slot] = sa; S.sb[slot] = sb; S.sc[slot] = sc; }
+    wave_fence();
+    if (pending) {
+        r.alw = S.xalw[lane] != 0;
+        r.rem = S.xrem[lane];
+        r.tok = S.xtok[lane];
+        n_allowed += r.alw ? 1u : 0u;
+        pending = false;
+    }
+    wave_fence();
+}
+#endif
+
+// Apply one group of up to 64 requests (lane order = arrival order; `valid` lanes only).
+// SP: the region may be sparse (unloaded buckets, tombstones); image regions (SP = false)
+// compile those checks out of the probe loop.
+template <class Codec, int ALGO, bool SP, class LdsT>
+__device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimiter& L,
+                                     uint32_t lane, const typename Codec::Rec& cur, bool valid,
+                                     uint32_t j, int64_t base, uint32_t pad, uint32_t& n_allowed,
+                                     uint32_t& n_invalid, uint32_t& n_caperr, uint32_t& n_rounds,
+                                     uint32_t& n_hits, SparseSrc& sp) {
+    constexpr uint32_t NS = kRegionSlots;
+    constexpr bool tb = ALGO == kAlgoTB;        // per-algorithm code: nothing of the other
+    constexpr bool CACHE = LdsT::kCache && !tb;
+    const bool cache_on = CACHE && L.cache_ttl_ms > 0;
+    Applied r;
+    r.j = valid ? j : pad;
+    const Req q = Codec::dec(cur, base);
+    const bool live = valid && !q.invalid;
+    r.alw = false;
+    r.rem = kRemInvalid;
+    r.tok = __builtin_nan("");
+    n_invalid += (valid && q.invalid) ? 1u : 0u;
+    // ---- find or insert the key's slot (lookup phase, then claim phase)
+    int32_t slot = -1;
+    bool need = live, failed = false;
+    const uint32_t home = slot_home(q.h);
+    if (a.ablate & kAblNoProbe) { if (need) slot = (int32_t)home; need = false; }
+    for (;;) {
+        if (!__any(need)) break;
+        uint32_t cand = kNone, fault = kNone;
+        bool cand_tomb = false;
+        if (need) {
+            // linear probing from a 4-aligned home, one 4-slot bucket per step: the key
+            // is in the chain before its first free slot (nothing is deleted mid-batch).
+            // A sparse region may reach a bucket not loaded yet (fault it in, retry) and
+            // holds tombstones (never a hit; the first one before the free slot is reused).
+            uint32_t p = home, tomb = kNone;
+            for (uint32_t step = 0; step < NS / 4; ++step) {
+                const uint4 o4 = *(const uint4*)&S.occ[p];
+                if (SP && (o4.x & kOccUnloaded)) {  // a bucket is loaded whole
+                    fault = p;
+                    sp.long_chain |= step >= 2;
+                    break;
+                }
+                const ulonglong2 t01 = *(const ulonglong2*)&S.tag[p];
+                const ulonglong2 t23 = *(const ulonglong2*)&S.tag[p + 2];
+                const uint32_t occm = (o4.x & 1u) | (o4.y & 1u) << 1 | (o4.z & 1u) << 2 |
+                                      (o4.w & 1u) << 3;
+                const uint32_t tombm = !SP ? 0u : (o4.x >> 3 & 1u) | (o4.y >> 3 & 1u) << 1 |
+                                                         (o4.z >> 3 & 1u) << 2 | (o4.w >> 3 & 1u) << 3;
+                const uint32_t hit = occm & ~tombm &
+                                     ((t01.x == q.h ? 1u : 0u) | (t01.y == q.h ? 2u : 0u) |
+                                      (t23.x == q.h ? 4u : 0u) | (t23.y == q.h ? 8u : 0u));
+                const uint32_t freem = ~occm & 15u;
+                // first free slot vs first hit in scan order
+                const uint32_t ff = freem ? (uint32_t)__builtin_ctz(freem) : 4u;
+                const uint32_t fh = hit ? (uint32_t)__builtin_ctz(hit) : 4u;
+                if (fh < ff) { slot = (int32_t)(p + fh); need = false; break; }
+                const uint32_t tm = tombm & ((1u << ff) - 1u);
+                if (tomb == kNone && tm) tomb = p + (uint32_t)__builtin_ctz(tm);
+                if (ff < 4u) {
+                    cand = tomb != kNone ? tomb : p + ff;
+                    cand_tomb = tomb != kNone;
+                    sp.long_chain |= step >= 2;
+                    break;
+                }
+                p = (p + 4) & (NS - 1);
+            }
+            if (need && cand == kNone && fault == kNone) {
+                if (tomb != kNone) { cand = tomb; cand_tomb = true; }   // wrapped: reuse a tombstone
+                else { need = false; failed = true; }
+            }
+        }
+        if (SP && __any(fault != kNone)) {
+            // lanes faulting the same bucket write the same words; nothing else in the
+            // wave touches an unloaded bucket
+            if (fault != kNone) fault_bucket(sp, L, S, fault);
+        }
+        wave_fence();
+        const uint32_t expect = cand_tomb ? (kOccUsed | kOccTomb) : 0u;
+        if (need && cand != kNone && atomicCAS(&S.occ[cand], expect, kOccUsed) == expect) {
+            S.tag[cand] = q.h; S.sa[cand] = 0; S.sb[cand] = 0; S.sc[cand] = 0;
+            if constexpr (LdsT::kCache) S.sx[cand] = 0;
+            slot = (int32_t)cand;
+            need = false;
+        }
+        wave_fence();
+    }
+    if (failed) {
+        r.rem = kRemError;
+        ++n_caperr;
+    }
+    if (slot >= 0) atomicOr(&S.occ[slot], 2u);
+    // ---- apply in arrival order. Per round, two hypotheses about a key's pending requests
+    // are tested at once against its current state: (D) every earlier one is denied (no
+    // state change: SlidingWindowRateLimiter.java:104-111, Lua :61-67) -> the prefix up to
+    // and including the first state-changing request is final; (A, sliding window only)
+    // every earlier one is allowed (the current bucket counts them: :114-116) -> the prefix
+    // up to and including the first denied request is final. The longer prefix is taken,
+    // so a run of denials or a run of allows costs one round, not one per request.
+    const bool one_round = (a.ablate & kAblNoRounds) != 0;
+    const uint64_t peers = one_round ? (1ULL << lane)
+                                     : wave_match((uint32_t)slot, kRegionBits, slot >= 0);
+    bool pending = slot >= 0;
+    SWGeo geo{};
+    uint64_t same_w = 0, elig_m = 0;        // (A): lanes in my window / acquires
+    if constexpr (!tb) {
+        if (slot >= 0) geo = sw_geo(q.now_ms, L);
+        // window index relative to the wave's first window (2 bits; 3 = "far")
+        int64_t wmin = slot >= 0 ? geo.curr_start : INT64_MAX;
+        for (int o = 32; o > 0; o >>= 1) {
+            const int64_t x = __shfl_xor(wmin, o, 64);
+            wmin = x < wmin ? x : wmin;
+        }
+        int64_t wi = slot >= 0 ? (geo.curr_start - wmin) / L.window_ms : 3;
+        if (wi > 3) wi = 3;
+        const uint64_t b0 = __ballot(wi & 1), b1 = __ballot(wi & 2);
+        same_w = ((wi & 1) ? b0 : ~b0) & ((wi & 2) ? b1 : ~b1);
+        elig_m = __ballot(slot >= 0 && wi < 3 && q.op == (uint32_t)kOpAcquire);
+    }
+    [[maybe_unused]] uint32_t my_rounds = 0;      // -DRL_CHAINS only
+    while (__any(pending)) {
+        // Chains: after two rounds, if every key still pending has changed state in (nearly)
+        // every round so far (runs of TB allows, SW allows across windows) and some key still
+        // has >= 4 requests pending, the rounds would go on finalizing one request per key
+        // each; the lowest pending lane of every key then applies the key's remaining
+        // requests itself, in arrival order (each a full exact step; a deny leaves the state
+        // as it is), instead of one wave round per state change.
+#ifdef RL_CHAINS
+        if (!CACHE && my_rounds >= 2 && !one_round) {
+            const uint64_t kp = peers & __ballot(pending);
+            const uint32_t fin = (uint32_t)__popcll(peers) - (uint32_t)__popcll(kp);
+            if (__all(!pending || fin <= 2u * my_rounds) && __any(pending && __popcll(kp) >= 4)) {
+                ++n_rounds;
+                wave_chains<Codec, ALGO>(S, L, lane, q, geo, slot, pending, kp, r, n_allowed);
+                break;
+            }
+        }
+#endif
+        ++my_rounds;
+        ++n_rounds;
+        Outcome o{};
+        SWAllow al{false, 0};
+        bool elig = false, hit = false, xs = false;
+        const uint64_t pm = __ballot(pending);
+        const uint64_t kp = peers & pm;                        // my key's pending requests
+        if (pending) {
+            const uint64_t sa = S.sa[slot], sb = S.sb[slot], sc = S.sc[slot];
+            if (a.ablate & kAblNoStep) {
+                o.mutate = (q.permits & 1) != 0; o.allowed = o.mutate; o.remaining = q.permits;
+                o.a = sa; o.b = sb; o.c = sc;
+            } else {
+                if constexpr (tb) {
+                    o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
+                } else if (cache_on) {
+                    if constexpr (CACHE) {
+                        const uint64_t x0 = S.sx[slot];
+                        o = sw_step_cache(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc, x0, hit);
+                        // (A) with the local cache: while the key has no cache entry that
+                        // rejects (x0 == 0) a put changes nothing unless its value reaches
+                        // max (:106-108, :119-121), so a run of allows is still closed-form;
+                        // the request whose put sets the entry (xs) ends the run, inclusive
+                        const uint64_t upto = kp & (((1ULL << lane) - 1) | (1ULL << lane));
+                        elig = x0 == 0 && (upto & ~(elig_m & same_w)) == 0 &&
+                               (int64_t)sa <= geo.curr_start && geo.prev_start != geo.curr_start;
+                        if (elig) {
+                            const uint32_t k = popc_below(kp);
+                            al = sw_try_after_allows(L, q.permits, q.now_ms, geo, sa, sb, sc, k);
+                            const SW2 s0 = sw_unpack(sa, sb, sc);
+                            const int64_t curr0 = s0.b1_start == geo.curr_start ? (int64_t)s0.b1_cnt : 0;
+                            // allow: newCount = curr0 + k + 1; deny: the estimate, >= max iff
+                            // its remaining is 0
+                            xs = al.allowed ? curr0 + (int64_t)k + 1 >= L.max_permits : al.remaining == 0;
+                        }
+                    }
+                } else {
+                    o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, sa, sb, sc);
+                    // (A) for this request needs: it and every EARLIER pending peer are
+                    // acquires in its window, not before the key's newest bucket (the allows
+                    // of one window then only INCR its bucket). A later window's requests
+                    // become eligible in the next round, once this window's are final.
+                    const uint64_t upto = kp & (((1ULL << lane) - 1) | (1ULL << lane));
+                    // (near the epoch, now < w, Java's truncating division makes the previous
+                    // window the current one, :170-172: its count then moves with the allows)
+                    elig = (upto & ~(elig_m & same_w)) == 0 && (int64_t)sa <= geo.curr_start &&
+                           geo.prev_start != geo.curr_start;
+                    if (elig) al = sw_try_after_allows(L, q.permits, q.now_ms, geo, sa, sb, sc,
+                                                       popc_below(kp));
+                }
+            }
+        }
+        const uint64_t mut = __ballot(pending && o.mutate) & peers;
+        const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
+        bool use_a = false;
+        uint32_t fa = 64u, a_end = 0u;
+        if constexpr (!tb) {
+            // per key: (A) is final up to its first denial (inclusive) or its first pending
+            // request that is not eligible (exclusive); (D) up to the first state change
+            const uint64_t den = __ballot(pending && elig && (!al.allowed || xs)) & peers;
+            const uint64_t nel = __ballot(pending && !elig) & peers;
+            const uint32_t fd = den ? (uint32_t)__builtin_ctzll(den) : 64u;
+            const uint32_t fs = nel ? (uint32_t)__builtin_ctzll(nel) : 64u;
+            fa = fd < fs ? fd : fs;                 // allows: the pending peers below fa
+            a_end = fd < fs ? fd + 1u : fs;
+            // (cache) the run's last request is itself an allow when its put sets the entry
+            if (fd < fs && ((__ballot(pending && elig && al.allowed && xs) & peers) >> fd & 1u)) fa = fd + 1u;
+            const uint32_t d_end = fm < 64u ? fm + 1u : 64u;
+            use_a = a_end > d_end;               // the allow hypothesis decides more
+        }
+        if (pending && use_a) {
+            if constexpr (!tb) {
+                if (lane < a_end) {
+                    const uint64_t ok = kp & (fa >= 64u ? ~0ULL : ((1ULL << fa) - 1));   // the allows
+                    if (ok && lane == 63u - (uint32_t)__builtin_clzll(ok)) {   // the last allow commits
+                        uint64_t na = S.sa[slot], nb = S.sb[slot], nc = S.sc[slot];
+                        sw_commit_allows(L, geo, na, nb, nc, (uint32_t)__popcll(ok), q.now_ms);
+                        S.sa[slot] = na; S.sb[slot] = nb; S.sc[slot] = nc;
+                    }
+                    if constexpr (CACHE)
+                        if (xs && lane + 1u == a_end)        // this request's put sets the entry
+                            S.sx[slot] = (uint64_t)(q.now_ms + L.cache_ttl_ms);
+                    r.alw = al.allowed;
+                    r.rem = al.remaining;
+                    r.tok = __builtin_nan("");
+                    n_allowed += al.allowed ? 1u : 0u;
+                    pending = false;
+                }
+            }
+        } else if (pending && lane <= fm) {
+            if (lane == fm) {
+                S.sa[slot] = o.a; S.sb[slot] = o.b; S.sc[slot] = o.c;
+                if constexpr (CACHE) if (cache_on) S.sx[slot] = o.x;
+            }
+            r.alw = o.allowed;
+            r.rem = o.remaining;
+            r.tok = o.tokens;
+            n_allowed += o.allowed ? 1u : 0u;
+            n_hits += hit ? 1u : 0u;                   // counted once, when final
+            pending = false;
+        }
+        wave_fence();
+    }
+    return r;
+}
+
+template <class Codec, class Res, bool TOK, int BS, class LdsT>
+__device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
+    using Rec = typename Codec::Rec;
+    constexpr uint32_t NS = kRegionSlots;
+    constexpr uint32_t RPB = 1u << BS;              // regions per bin
+
+    // RPB = 8: block g = 64q + 8r + x  ->  bin 8q + x, region r of that bin (see above)
+    const uint32_t bin = RPB == 1 ? g : (g / 64) * 8 + (g % 8);
+    const uint32_t rb = RPB == 1 ? 0u : (g / 8) % 8;
+    const uint32_t n_bins = a.n_regions / RPB;
+    if (bin >= n_bins) return;
+    if (a.hot_mark && a.hot_mark[bin] == a.epoch) return;     // owned by hot_chain
+    if (a.ablate & kAblNoNormal) return;
+    const uint32_t start = a.rstart[bin];
+    const uint32_t cnt = a.rend ? a.rend[bin] - start : a.rcount[bin];
+    if (cnt == 0) return;
+    const uint32_t end = start + cnt;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t region = bin * RPB + rb;
+    const DevLimiter L = a.lims[a.region_lim[region]];
+    const int64_t base = a.ctl->base_ms;
+    const int64_t batch_min = keep_from(a);
+    const uint32_t pad = a.n_total + lane;          // padding slot for idle lanes
+    const Rec* recs = (const Rec*)a.rec;
+    Res* res = (Res*)a.res;
+
+    if (a.ctl->span_overflow != 0) {
+        // compact records cannot represent this batch's time span: reject it whole,
+        // before any state is touched (the host reports RL_E_INVALID_ARG). Wave rb of
+        // the bin writes its region's share.
+        for (uint32_t j = start + lane; j < end; j += 64) {
+            const Rec r = recs[j];
+            if ((region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb) {
+                res[j] = (Res)pack_result(false, kRemInvalid);
+                if (TOK) a.tok[j] = __builtin_nan("");
+            }
+        }
+        return;
+    }
+    // kDepth slices of the bin's stream in flight (issued while the region image loads)
+    constexpr uint32_t kDepth = 4;
+    // unconditional; read once when the bin is the region (streaming), else shared by RPB waves
+    auto fetch = [&](uint32_t c) { return ld_rec<kNtRgRec && RPB == 1>(recs + min(c + lane, end - 1)); };
+    Rec q0 = fetch(start), q1 = fetch(start + 64), q2 = fetch(start + 128), q3 = fetch(start + 192);
+
+    // ---- load the region, dropping entries no request of this batch can see, and
+    // rebuild its open-addressing table (no tombstones ever reach HBM)
+    Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
+    uint64_t* xtab = nullptr;                       // the slots' local-cache states
+    if constexpr (LdsT::kCache)
+        if (L.cache_table) xtab = (uint64_t*)L.cache_table + (size_t)(region - L.region_base) * NS;
+    // Few records: probe and update single buckets in HBM (128 B read + 32 B written per
+    // distinct key) instead of moving the 8 KB image both ways.
+    const bool sparse = kSparseOn && RPB == 1 && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
+    SparseSrc sp{sparse ? tab : nullptr, xtab, batch_min, false};
+    // rebuild the LDS table from registers: linear probing from each key's home
+    auto rebuild = [&](const Slot (&img)[NS / 64], const uint64_t (&xim)[NS / 64], const bool (&keep)[NS / 64]) {
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) S.occ[lane + 64 * i] = 0;
+        wave_fence();
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) {
+            const Slot v = img[i];
+            if (keep[i]) {
+                uint32_t p = slot_home(v.tag);
+                while (atomicCAS(&S.occ[p], 0u, 1u) != 0u) p = (p + 1) & (NS - 1);
+                S.tag[p] = v.tag; S.sa[p] = v.a; S.sb[p] = v.b; S.sc[p] = v.c;
+                if constexpr (LdsT::kCache) S.sx[p] = xim[i];
+            }
+        }
+        wave_fence();
+    };
+    if (sparse) {
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) S.occ[lane + 64 * i] = kOccUnloaded;
+        wave_fence();
+    } else {
+        // load the region, dropping entries no request of this batch can see
+        Slot img[NS / 64];
+        uint64_t xim[NS / 64];
+        bool keep[NS / 64];
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) {
+            img[i] = tab[lane + 64 * i];
+            xim[i] = xtab ? xtab[lane + 64 * i] : 0;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) keep[i] = slot_live(L, img[i], batch_min, xim[i]);
+        rebuild(img, xim, keep);
+    }
+
+    uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_hits = 0;
+    const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t head = 0, count = 0;                    // ring state (wave-uniform)
+    // the whole stream is instantiated once per algorithm (uniform per region), so the
+    // compiler hoists nothing of the other algorithm into the hot loop
+    auto stream = [&](auto algo, auto spc) {
+        constexpr int A = decltype(algo)::value;
+        constexpr bool SPX = decltype(spc)::value;
+        auto slice = [&](const Rec& r, uint32_t c0) {
+            const uint32_t idx = c0 + lane;
+            if constexpr (RPB == 1) {
+                // the bin is the region: every record is ours, applied straight from registers
+                const Applied ap = wave_apply<Codec, A, SPX>(a, S, L, lane, r, idx < end, idx, base, pad,
+                                                     n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
+                put_res<Res>(a, ap.j, ap.alw, ap.rem);
+                if (TOK) a.tok[ap.j] = ap.tok;
+            } else {
+                const bool mine = idx < end &&
+                    (region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb;
+                const uint64_t bal = __ballot(mine);
+                if (mine) {
+                    const uint32_t k = (head + count + popc_below(bal)) % kRing;
+                    S.ring[k] = r;
+                    S.ring_pos[k] = idx;
+                }
+                count += (uint32_t)__popcll(bal);
+                wave_fence();
+                Applied ap;
+                ap.j = pad; ap.alw = false; ap.rem = kRemError; ap.tok = 0.0;
+                if (count >= 64) {
+                    const uint32_t ri = (head + lane) % kRing;
+                    ap = wave_apply<Codec, A, SPX>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
+                                           n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
+                    head = (head + 64) % kRing;
+                    count -= 64;
+                }
+                put_res<Res>(a, ap.j, ap.alw, ap.rem);   // exactly one store per slice
+                if (TOK) a.tok[ap.j] = ap.tok;
+            }
+        };
+        // unrolled by kDepth so the prefetch registers rotate without moves (a register move
+        // would wait on its load and shrink the effective depth to one slice)
+        for (uint32_t c0 = start; c0 < end; c0 += 64 * kDepth) {
+            slice(q0, c0);
+            q0 = fetch(c0 + 64 * kDepth);
+            if (c0 + 64 >= end) break;
+            slice(q1, c0 + 64);
+            q1 = fetch(c0 + 64 * kDepth + 64);
+            if (c0 + 128 >= end) break;
+            slice(q2, c0 + 128);
+            q2 = fetch(c0 + 64 * kDepth + 128);
+            if (c0 + 192 >= end) break;
+            slice(q3, c0 + 192);
+            q3 = fetch(c0 + 64 * kDepth + 192);
+        }
+        if constexpr (RPB > 1) {
+            if (count > 0) {
+                const bool v = lane < count;
+                const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
+                const Applied ap = wave_apply<Codec, A, SPX>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
+                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
+                put_res<Res>(a, ap.j, ap.alw, ap.rem);
+                if (TOK) a.tok[ap.j] = ap.tok;
+            }
+        }
+    };
+    using SpOn = std::integral_constant<bool, kSparseOn && RPB == 1>;
+    using SpOff = std::integral_constant<bool, false>;
+    if (L.algo == kAlgoTB) {
+        if (sparse) stream(std::integral_constant<int, kAlgoTB>{}, SpOn{});
+        else stream(std::integral_constant<int, kAlgoTB>{}, SpOff{});
+    } else {
+        if (sparse) stream(std::integral_constant<int, kAlgoSW>{}, SpOn{});
+        else stream(std::integral_constant<int, kAlgoSW>{}, SpOff{});
+    }
+    wave_fence();
+    uint32_t touched = 0;
+    for (uint32_t s = lane; s < NS; s += 64) touched += (S.occ[s] & kOccTouched) ? 1u : 0u;
+    bool whole = !sparse;
+    if (sparse && __any(sp.long_chain)) {
+        // probe chains have grown long (tombstones accumulate while a region only ever sees
+        // few records): fault in the rest of the region (one bucket per lane), keep its live
+        // keys and rebuild it as an image region does, then write it back whole
+        if (S.occ[4 * lane] & kOccUnloaded) fault_bucket(sp, L, S, 4 * lane);
+        wave_fence();
+        Slot img[NS / 64];
+        uint64_t xim[NS / 64];
+        bool keep[NS / 64];
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) {
+            const uint32_t s = lane + 64 * i;
+            const uint32_t o = S.occ[s];
+            keep[i] = (o & kOccUsed) && !(o & kOccTomb);
+            img[i] = Slot{S.tag[s], S.sa[s], S.sb[s], S.sc[s]};
+            xim[i] = 0;
+            if constexpr (LdsT::kCache) xim[i] = S.sx[s];
+        }
+        wave_fence();
+        rebuild(img, xim, keep);
+        whole = true;
+    }
+    // ---- write the region back: every slot (free ones as zeros), or in a sparse region
+    // only the slots this batch touched
+    uint32_t used = 0;                               // live keys (whole regions only)
+    uint32_t moved = 0;                              // table bytes read + written (sparse)
+    const uint32_t xw = xtab ? 8u : 0u;              // local-cache word per slot
+    for (uint32_t s = lane; s < NS; s += 64) {
+        const uint32_t o = S.occ[s];
+        used += (whole && (o & kOccUsed) && !(o & kOccTomb)) ? 1u : 0u;
+        if (!whole) moved += (!(o & kOccUnloaded) && (s & 3u) == 0 ? 4u * (32u + xw) : 0u) +
+                             ((o & kOccTouched) ? 32u + xw : 0u);
+        if (!whole && !(o & kOccTouched)) continue;
+        Slot v{0, 0, 0, 0};
+        uint64_t x = 0;
+        if (o & kOccUsed) {
+            if constexpr (LdsT::kCache) x = S.sx[s];
+            v = slot_used(Slot{S.tag[s], S.sa[s], S.sb[s], S.sc[s]}, x);
+        }
+        tab[s] = v;
+        if constexpr (LdsT::kCache)
+            if (xtab) xtab[s] = x;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        n_allowed += __shfl_xor(n_allowed, off, 64);
+        n_invalid += __shfl_xor(n_invalid, off, 64);
+        n_caperr += __shfl_xor(n_caperr, off, 64);
+        n_hits += __shfl_xor(n_hits, off, 64);
+        touched += __shfl_xor(touched, off, 64);
+        used += __shfl_xor(used, off, 64);
+        moved += __shfl_xor(moved, off, 64);
+    }
+    if (lane == 0) {
+        note_fill(a, region, used, n_caperr != 0);
+        unsigned long long* st = a.stats + (size_t)(blockIdx.x & (kStatSlots - 1)) * kStWords;
+        atomicAdd(st + kStTableBytes, whole ? (unsigned long long)(2u * NS * (32u + xw))
+                                            : (unsigned long long)moved);
+        if (n_allowed) atomicAdd(st + kStAllowed, (unsigned long long)n_allowed);
+        if (n_invalid) atomicAdd(st + kStInvalid, (unsigned long long)n_invalid);
+        if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
+        atomicAdd(st + kStDistinct, (unsigned long long)touched);
+        atomicAdd(st + kStRegions, 1ULL);
+        if (n_hits) atomicAdd(st + kStCacheHits, (unsigned long long)n_hits);
+        if (a.dbg) {
+            uint64_t* d = a.dbg + (size_t)bin * kDbgWords;
+            d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = cnt; d[3] = n_rounds;
+        }
+    }
+}
+
+#ifndef RL_HOT_MIN_WAVES
+#define RL_HOT_MIN_WAVES 4
+#endif
+// Normal regions (one wave each) at >= RL_REGION_MIN_WAVES waves per SIMD (VGPR budget).
+#ifndef RL_REGION_MIN_WAVES
+#define RL_REGION_MIN_WAVES 4
+#endif
+
+}  // namespace rl

@@ -1,0 +1,7 @@
+// Normal-region kernels for CodecW records with uint64_t packed results.
+#include "rl_region_k.hpp"
+
+namespace rl {
+template hipError_t region_launch_t<CodecW, uint64_t>(const RegionArgs&, hipStream_t, hipStream_t,
+                                                     hipEvent_t, hipEvent_t);
+}  // namespace rl
