@@ -60,6 +60,7 @@ struct BatchScratch {
     void* rec1 = nullptr;
     uint32_t* pos0 = nullptr;
     uint32_t* pos1 = nullptr;
+    uint16_t* digit = nullptr;              // routing: pass-0 digit per request
     void* res = nullptr;
     int64_t* ext = nullptr;                 // escaped remainders (kResEscape), like res
     double* tok = nullptr;
@@ -109,6 +110,18 @@ struct rl_engine {
     size_t hot_mark_cap = 0;
     uint32_t epoch = 0;
     uint32_t hot_threshold = 16384;         // rl_tune("hot_threshold"); 0 disables
+    // Hot-region routing (two-pass batches): the previous batch's hot regions get pass-0 bins
+    // of their own and skip pass 1. route_list holds region ids (kNone = unused); it is built
+    // on device at the end of each batch's hot preparation and cleared when region ids change.
+    bool route = true;                      // rl_tune("route")
+    bool region_order = true;               // rl_tune("region_order"): largest regions dispatched first
+    uint32_t order_prefix = 4096;           // rl_tune("order_prefix"): ... after this many of the smallest
+    uint32_t* order = nullptr;              // [order_cap + 1]
+    size_t order_cap = 0;
+    uint32_t* order_meta = nullptr;         // [kOrderMeta]
+    uint32_t* route_list = nullptr;         // [kRouteSlots] table of region ids (kNone = empty)
+    uint32_t* route_start = nullptr;        // [kRouteSlots] this batch's routed bins
+    uint32_t* route_cnt = nullptr;          // [kRouteSlots]
     uint32_t sparse_max = 96;               // rl_tune("sparse_max"): records per region up to
                                             // which a region probes single buckets; 0 = never
     uint64_t* dbg = nullptr;                // rl_tune("debug_regions"): per-bin stamps
@@ -279,6 +292,12 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
     if (rc == RL_OK) rc = dalloc(&e->hot_list, kHotListWords);
     if (rc == RL_OK) rc = dalloc(&e->hot_info, kHotMax);
+    if (rc == RL_OK) rc = dalloc(&e->route_list, kRouteSlots);
+    if (rc == RL_OK) rc = dalloc(&e->route_start, kRouteSlots);
+    if (rc == RL_OK) rc = dalloc(&e->route_cnt, kRouteSlots);
+    if (rc == RL_OK) rc = dalloc(&e->order_meta, kOrderMeta);
+    if (rc == RL_OK && hipMemset(e->route_list, 0xFF, kRouteSlots * sizeof(uint32_t)) != hipSuccess)
+        rc = RL_E_DEVICE;
     if (rc != RL_OK) { rl_destroy(e); return rc; }
     std::memset(e->h_ctl, 0, sizeof(BatchCtl));
     *out = e;
@@ -294,7 +313,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->d_lims); dfree(e->d_region_lim);
     for (BatchScratch& B : e->sc) {
         dfree(B.rec0); dfree(B.rec1); dfree(B.pos0); dfree(B.pos1); dfree(B.res); dfree(B.tok);
-        dfree(B.ext);
+        dfree(B.ext); dfree(B.digit);
         dfree(B.counts); dfree(B.bin_total); dfree(B.bin_base);
         dfree(B.region_count); dfree(B.region_start);
         dfree(B.d_ctl);
@@ -302,6 +321,8 @@ extern "C" void rl_destroy(rl_engine* e) {
         if (B.freed) (void)hipEventDestroy(B.freed);
     }
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
+    dfree(e->route_list); dfree(e->route_start); dfree(e->route_cnt);
+    dfree(e->order); dfree(e->order_meta);
     dfree(e->d_stats); dfree(e->d_work);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
@@ -435,6 +456,8 @@ static int grow_once(rl_engine* e, size_t li) {
     for (auto& l : e->lims) { l.dev.region_base = base; base += 1u << l.dev.region_bits; }
     e->n_regions = base;
     ++e->grows;
+    // region ids changed: the next batch routes nothing (its hot preparation lists anew)
+    HIP_OK(hipMemset(e->route_list, 0xFF, kRouteSlots * sizeof(uint32_t)));
     return upload_limiters(e);
 }
 
@@ -469,8 +492,9 @@ static int ensure_scratch(rl_engine* e, BatchScratch& B, size_t n, bool wide, ui
         const size_t rb = wide ? sizeof(RecW) : sizeof(RecC);
         const size_t padn = cap + kTileThreads;   // kernels write inactive lanes past n
         dfree(B.rec0); dfree(B.rec1); dfree(B.pos0); dfree(B.pos1); dfree(B.res); dfree(B.tok);
-        dfree(B.ext);
+        dfree(B.ext); dfree(B.digit);
         int rc = dalloc(&B.rec0, padn * rb);
+        if (rc == RL_OK) rc = dalloc(&B.digit, padn);
         if (rc == RL_OK) rc = dalloc(&B.rec1, padn * rb);
         if (rc == RL_OK) rc = dalloc(&B.pos0, padn);
         if (rc == RL_OK) rc = dalloc(&B.pos1, padn);
@@ -565,6 +589,11 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
     const int d0 = passes == 1 ? bitsP : bitsP - bitsP / 2;
     const int d1 = bitsP - d0;
+    // hot-region routing: pass 0 gets kRouteSlots bins beyond the 2^d0 low-digit ones
+    const bool hot_on = e->hot_threshold > 0 && !cache && e->bin_shift == 0;
+    const bool route = hot_on && e->route && passes == 2 && !e->pipeline &&
+                       (1u << d0) + kRouteSlots <= (1u << kMaxDigitBits);
+    const uint32_t nb0 = route ? (1u << d0) + kRouteSlots : 1u << d0;
     // Scratch set and partition stream. With RL_OPT_PIPELINE the partition (stages 1-3)
     // runs on e->pstream into one of two scratch sets, so batch k+1's partition overlaps
     // batch k's region stage; the region stage and the unpermute stay on e->stream (state
@@ -574,14 +603,14 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     const int set = e->pipeline ? e->next_set : 0;
     BatchScratch& B = e->sc[set];
     hipStream_t ps = e->pipeline ? e->pstream : s;
-    const size_t need_counts = (size_t)(1u << std::max(d0, d1)) * nt;
+    const size_t need_counts = (size_t)std::max<uint32_t>(nb0, 1u << d1) * nt;
     if (e->pipeline && (n > B.cap_n || (wide && !B.cap_wide) || need_counts > B.counts_cap ||
                         (passes == 2 && n_bins > B.region_cap))) {
         // growing a set frees its old buffers: nothing may still be using them
         HIP_OK(hipStreamSynchronize(s));
         HIP_OK(hipStreamSynchronize(ps));
     }
-    int rc = ensure_scratch(e, B, n, wide, 1u << std::max(d0, d1), nt);
+    int rc = ensure_scratch(e, B, n, wide, std::max<uint32_t>(nb0, 1u << d1), nt);
     if (rc != RL_OK) return rc;
     if (passes == 2) {
         rc = ensure_regions(B, n_bins);
@@ -616,16 +645,25 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.counts = B.counts; pa.bin_base = B.bin_base; pa.ablate = e->ablate;
     pa.bin_shift = bsh;
     pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu;
-    // ---- pass 0 (low digit) from the caller's arrays
-    pa.digit_shift = 0; pa.digit_bits = d0;
+    // ---- pass 0 (low digit) from the caller's arrays; routed hot regions get bins
+    // 2^d0 + slot and their records go straight to the final array (rec1)
+    pa.digit_shift = 0; pa.digit_bits = route ? ceil_log2(nb0) : d0;
+    pa.n_bins_pass = nb0;
     pa.region_count = nullptr;
     pa.rec_out = B.rec0; pa.pos_out = B.pos0;
+    if (route) {
+        pa.route_list = e->route_list; pa.lo_bins = 1u << d0; pa.rec_out_route = B.rec1;
+        pa.digit = B.digit;
+    }
     HIP_OK(launch_upsweep(pa, true, wide, ps));
     mark_on(e, ps, 1);
-    HIP_OK(launch_scan_rows(B.counts, B.counts, 1u << d0, nt, B.bin_total, ps));
-    HIP_OK(launch_scan_small(B.bin_total, B.bin_base, 1u << d0, ps));
+    HIP_OK(launch_scan_rows(B.counts, B.counts, nb0, nt, B.bin_total, ps));
+    HIP_OK(launch_scan_small(B.bin_total, B.bin_base, nb0, ps));
     mark_on(e, ps, 2);
     HIP_OK(launch_scatter(pa, true, wide, ps));
+    if (route)
+        HIP_OK(launch_route_ranges(B.bin_base, B.bin_total, 1u << d0, e->route_start, e->route_cnt,
+                                   B.d_ctl, ps));
     mark_on(e, ps, 3);
     const void* rec_final = B.rec0;
     const uint32_t* rstart = B.bin_base;
@@ -635,6 +673,9 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         // ---- pass 1 (high digit) over the records; stable, so the final order is
         // bin-major and arrival-ordered inside each bin.
         pa.digit_shift = d0; pa.digit_bits = d1;
+        pa.n_bins_pass = 1u << d1;
+        pa.route_list = nullptr; pa.digit = nullptr;
+        pa.n_dev = route ? &B.d_ctl->n_normal : nullptr;  // routed records stay where pass 0 put them
         pa.rec_in = B.rec0; pa.rec_out = B.rec1; pa.pos_out = B.pos1;
         HIP_OK(launch_upsweep(pa, false, wide, ps));
         mark_on(e, ps, 4);
@@ -691,13 +732,28 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (hot) {
         uint32_t* hot_count = e->hot_list + kHotMax;
         HIP_OK(hipMemsetAsync(hot_count, 0, kHotMetaWords * sizeof(uint32_t), s));
+        if (route) HIP_OK(launch_hot_route_list(e->route_list, e->route_cnt, e->hot_list, hot_count, s));
         HIP_OK(launch_hot_select(rstart, rcount, rend, n_bins, e->hot_threshold, e->hot_list,
                                  hot_count, e->hot_mark, e->epoch, s));
         ra.hot_list = e->hot_list; ra.hot_count = hot_count; ra.hot_mark = e->hot_mark;
         ra.epoch = e->epoch;
         ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ;
         ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 4; ra.hot_total = e->hot_list + kHotMax + kHotTotalOff;
+        ra.route_list = e->route_list; ra.route_start = e->route_start; ra.route_cnt = e->route_cnt;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
+        // the next batch's routed regions: this batch's largest hot regions (two-pass tables)
+        if (e->route && passes == 2 && !e->pipeline)
+            HIP_OK(launch_route_next(e->hot_info, hot_count, e->hot_threshold, e->route_list, s));
+    }
+    if (e->region_order && bsh == 0) {
+        if (e->order_cap < n_bins) {
+            dfree(e->order);
+            if (dalloc(&e->order, (size_t)n_bins + 1) != RL_OK) { e->order_cap = 0; return RL_E_NOMEM; }
+            e->order_cap = n_bins;
+        }
+        HIP_OK(launch_region_order(rstart, rcount, rend, n_bins, e->order_meta, e->order, s));
+        ra.order = e->order;
+        ra.order_prefix = e->order_prefix;
     }
     mark(e, 7);
     // hot chains first (side stream), then the regions
@@ -985,6 +1041,19 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "region_walk") == 0) {       // 0 = one workgroup per region
         if (value < 0 || value > 32) return RL_E_INVALID_ARG;
         e->region_walk = (uint32_t)value;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "region_order") == 0) {
+        e->region_order = value != 0;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "order_prefix") == 0) {
+        if (value < 0) return RL_E_INVALID_ARG;
+        e->order_prefix = (uint32_t)value;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "route") == 0) {             // hot-region routing in pass 0
+        e->route = value != 0;
         return RL_OK;
     }
     if (std::strcmp(key, "split_hot") == 0) {

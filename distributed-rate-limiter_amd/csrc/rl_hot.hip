@@ -94,12 +94,14 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
                                                     uint32_t epoch) {
     __shared__ uint32_t s_thr;
     __shared__ uint32_t s_off[33];                    // list offset of each size class
+    // routed regions (k_hot_route_list) hold the first entries of the list
+    const uint32_t routed = hot_meta[kHotRoutedOff];
     if (threadIdx.x == 0) {
         uint32_t above = 0, thr = 0xFFFFFFFFu;
         for (int c = 32; c >= 0; --c) {               // classes from the largest down
             s_off[c] = above;
             above += hot_meta[1 + c];
-            if (above > kHotMax) break;
+            if (above > kHotMax - routed) break;
             thr = c == 0 ? 1u : (1u << c);
         }
         s_thr = thr > threshold ? thr : threshold;
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
     // largest size class first: the chains' workgroups are dispatched in list order, and the
     // longest chains must not be the ones that wait for a slot beside the normal regions
     const uint32_t c = 31u - (uint32_t)__builtin_clz(cnt);
-    const uint32_t k = s_off[c] + atomicAdd(&hot_meta[kHotClassCursor + c], 1u);
+    const uint32_t k = routed + s_off[c] + atomicAdd(&hot_meta[kHotClassCursor + c], 1u);
     atomicAdd(&hot_meta[0], 1u);
     if (k < kHotMax) {                                // (always, by the choice of s_thr)
         hot_list[k] = b;
@@ -120,6 +122,146 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
     }
 }
 
+
+// Routed regions first in the hot list, every slot that received records (nothing else sees
+// them: their records skipped the normal partition), largest first (a size-class counting
+// sort: the longest chains are dispatched first). hot_meta[0] and [kHotRoutedOff] = count.
+__global__ __launch_bounds__(1024) void k_hot_route_list(const uint32_t* __restrict__ route_list,
+                                                         const uint32_t* __restrict__ route_cnt,
+                                                         uint32_t* hot_list, uint32_t* hot_meta) {
+    __shared__ uint32_t s_cls[33], s_base[33];
+    static_assert(kRouteSlots == 2 * 1024, "two slots per thread");
+    const uint32_t t = threadIdx.x;
+    if (t < 33) s_cls[t] = 0;
+    __syncthreads();
+    uint32_t cls[2], k[2];
+    bool has[2];
+    for (int u = 0; u < 2; ++u) {
+        const uint32_t sl = t + 1024u * u;
+        const uint32_t c = route_cnt[sl];
+        has[u] = route_list[sl] != kNone && c > 0;
+        cls[u] = has[u] ? 31u - (uint32_t)__builtin_clz(c) : 0u;
+        k[u] = has[u] ? atomicAdd(&s_cls[cls[u]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t above = 0;
+        for (int c = 32; c >= 0; --c) { s_base[c] = above; above += s_cls[c]; }
+        hot_meta[0] = above;
+        hot_meta[kHotRoutedOff] = above;
+    }
+    __syncthreads();
+    for (int u = 0; u < 2; ++u)
+        if (has[u]) hot_list[s_base[cls[u]] + k[u]] = kHotRoutedBit | (t + 1024u * u);
+}
+
+// The next batch's route table: this batch's listed hot regions with >= threshold records,
+// largest first (ties by list position), each placed at the first free one of its two slots
+// (route_slots) by one thread; at most kRouteMax, a region whose slots are both taken stays
+// unrouted (it is then partitioned normally and found by the hot selection).
+__global__ __launch_bounds__(1024) void k_route_next(const HotInfo* __restrict__ info,
+                                                     const uint32_t* __restrict__ hot_count,
+                                                     uint32_t threshold, uint32_t* route_list) {
+    __shared__ uint32_t s_size[kHotMax];
+    __shared__ uint32_t s_rank[kHotMax];             // rank -> list index
+    __shared__ uint32_t s_tab[kRouteSlots];
+    const uint32_t hc = min(hot_count[0], kHotMax);
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < kHotMax; i += blockDim.x) {
+        s_size[i] = i < hc && info[i].end - info[i].start >= threshold ? info[i].end - info[i].start : 0u;
+        s_rank[i] = kNone;
+    }
+    for (uint32_t i = t; i < kRouteSlots; i += blockDim.x) s_tab[i] = kNone;
+    __syncthreads();
+    for (uint32_t i = t; i < hc; i += blockDim.x) {
+        const uint32_t si = s_size[i];
+        if (si == 0) continue;
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < hc; ++j) {
+            const uint32_t sj = s_size[j];
+            rank += (sj > si || (sj == si && j < i)) ? 1u : 0u;
+        }
+        s_rank[rank] = i;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t placed = 0;
+        for (uint32_t r = 0; r < hc && placed < kRouteMax; ++r) {
+            const uint32_t i = s_rank[r];
+            if (i == kNone) break;                   // ranks of eligible entries are dense
+            const uint32_t b = info[i].bin;
+            uint32_t s1, s2;
+            route_slots(b, s1, s2);
+            if (s_tab[s1] == kNone) { s_tab[s1] = b; ++placed; }
+            else if (s_tab[s2] == kNone) { s_tab[s2] = b; ++placed; }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < kRouteSlots; i += blockDim.x) route_list[i] = s_tab[i];
+}
+
+// Region dispatch order (launch_region_order): class c = floor(log2(records)) for non-empty
+// regions; classes are laid out largest first. meta[c] counts, meta[34 + c] cursors.
+__global__ __launch_bounds__(256) void k_order_count(const uint32_t* rstart, const uint32_t* rcount,
+                                                     const uint32_t* rend, uint32_t n_bins,
+                                                     uint32_t* meta) {
+    __shared__ uint32_t h[33];
+    if (threadIdx.x < 33) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b < n_bins) {
+        const uint32_t cnt = bin_records(rstart, rcount, rend, b);
+        if (cnt > 0) atomicAdd(&h[31 - __builtin_clz(cnt)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 33 && h[threadIdx.x]) atomicAdd(&meta[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_order_place(const uint32_t* rstart, const uint32_t* rcount,
+                                                     const uint32_t* rend, uint32_t n_bins,
+                                                     uint32_t* meta, uint32_t* order) {
+    __shared__ uint32_t s_base[33], s_cnt[33], s_blk[33];
+    const uint32_t t = threadIdx.x;
+    if (t == 0) {
+        uint32_t above = 0;
+        for (int c = 32; c >= 0; --c) { s_base[c] = above; above += meta[c]; }
+        if (blockIdx.x == 0) order[n_bins] = above;
+    }
+    if (t < 33) s_cnt[t] = 0;
+    __syncthreads();
+    const uint32_t b = blockIdx.x * 256 + t;
+    const uint32_t cnt = b < n_bins ? bin_records(rstart, rcount, rend, b) : 0u;
+    const uint32_t c = cnt ? 31u - (uint32_t)__builtin_clz(cnt) : 0u;
+    const uint32_t k = cnt ? atomicAdd(&s_cnt[c], 1u) : 0u;
+    __syncthreads();
+    if (t < 33 && s_cnt[t]) s_blk[t] = atomicAdd(&meta[34 + t], s_cnt[t]);   // one per class per block
+    __syncthreads();
+    if (cnt) order[s_base[c] + s_blk[c] + k] = b;
+}
+
+hipError_t launch_region_order(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
+                               uint32_t n_bins, uint32_t* meta, uint32_t* order, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(meta, 0, kOrderMeta * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const dim3 g((n_bins + 255) / 256), b(256);
+    hipLaunchKernelGGL(k_order_count, g, b, 0, s, rstart, rcount, rend, n_bins, meta);
+    hipLaunchKernelGGL(k_order_place, g, b, 0, s, rstart, rcount, rend, n_bins, meta, order);
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_route_list(const uint32_t* route_list, const uint32_t* route_cnt,
+                                 uint32_t* hot_list, uint32_t* hot_meta, hipStream_t s) {
+    hipLaunchKernelGGL(k_hot_route_list, dim3(1), dim3(1024), 0, s, route_list, route_cnt, hot_list,
+                       hot_meta);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_next(const HotInfo* hot_info, const uint32_t* hot_count, uint32_t threshold,
+                             uint32_t* route_list, hipStream_t s) {
+    hipLaunchKernelGGL(k_route_next, dim3(1), dim3(1024), 0, s, hot_info, hot_count, threshold,
+                       route_list);
+    return hipGetLastError();
+}
 
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s) {
     const dim3 gp(persistent_grid(1u << 30, 4));

@@ -160,9 +160,18 @@ __global__ __launch_bounds__(64) void k_hot_prep(RegionArgs a) {
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     const uint32_t i = blockIdx.x, lane = threadIdx.x;
     if (i >= hc) return;
-    const uint32_t bin = a.hot_list[i];
-    const uint32_t start = a.rstart[bin];
-    const uint32_t end = start + (a.rend ? a.rend[bin] - start : a.rcount[bin]);
+    const uint32_t e = a.hot_list[i];
+    uint32_t bin, start, end;
+    if (e & kHotRoutedBit) {                      // routed: its own pass-0 bin
+        const uint32_t r = e & ~kHotRoutedBit;
+        bin = a.route_list[r];
+        start = a.route_start[r];
+        end = start + a.route_cnt[r];
+    } else {
+        bin = e;
+        start = a.rstart[bin];
+        end = start + (a.rend ? a.rend[bin] - start : a.rcount[bin]);
+    }
     const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
     const int64_t base = a.ctl->base_ms;
     const uint32_t n0 = min(end - start, 64u);

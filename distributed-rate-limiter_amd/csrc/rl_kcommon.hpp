@@ -212,6 +212,31 @@ __device__ inline uint32_t bin_of(const PartArgs& a, uint32_t i, const LimLds& L
     return (L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift;
 }
 
+// Routed regions (pass 0): the route table (kRouteSlots region ids) in LDS; a region is
+// routed iff it sits at one of its two slots (route_slots), and that slot is its bin.
+struct RouteLds {
+    uint32_t key[kRouteSlots];
+};
+__device__ inline void route_load(RouteLds& R, const uint32_t* table) {
+    for (uint32_t s = threadIdx.x; s < kRouteSlots; s += blockDim.x) R.key[s] = table[s];
+    __syncthreads();
+}
+__device__ inline uint32_t route_find(const RouteLds& R, uint32_t b) {
+    uint32_t s1, s2;
+    route_slots(b, s1, s2);
+    const uint32_t k1 = R.key[s1], k2 = R.key[s2];         // independent reads
+    return k1 == b ? s1 : k2 == b ? s2 : kNone;
+}
+// Partition digit of global bin g in this pass: routed region -> lo_bins + slot, else
+// the low digit (pass 0 with routing); otherwise the digit at digit_shift.
+__device__ inline uint32_t pass_digit(const PartArgs& a, uint32_t g, const RouteLds& R) {
+    if (a.route_list) {
+        const uint32_t rs = route_find(R, g);
+        return rs != kNone ? a.lo_bins + rs : (g & (a.lo_bins - 1));
+    }
+    return (g >> a.digit_shift) & ((1u << a.digit_bits) - 1);
+}
+
 // first probe position of a key inside its region (4-slot aligned: probing reads buckets)
 __device__ inline uint32_t slot_home(uint64_t h) { return (uint32_t)h & (kRegionSlots - 4); }
 __device__ inline void wave_fence() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }

@@ -38,6 +38,9 @@ struct BatchCtl {
     unsigned long long cache_hits; // SW local-cache rejections (ratelimiter.cache.hits)
     unsigned long long grow[4];    // limiter bit set: one of its regions is filling up
     unsigned long long table_bytes;// state-table bytes read + written by the region stage
+    uint32_t n_normal;         // records in the normal partition: pass 0 routes the previous
+                               // batch's hot regions to bins of their own (k_route_ranges)
+    uint32_t pad1;
 };
 // A region holding more than kGrowUsed live keys after a batch (or one that overflowed)
 // flags its limiter for growth (rl_engine doubles its region count at the next status
@@ -73,6 +76,18 @@ struct PartArgs {
     uint32_t* region_count;    // nullable: full-region histogram (multi-pass only)
     BatchCtl* ctl;
     uint32_t ablate;           // rl_tune("ablate"): measurement-only variants (0 = product)
+    uint32_t n_bins_pass;      // bins of this pass (0: 1 << digit_bits)
+    // Hot-region routing (pass 0 of a two-pass batch): route_list is a kRouteSlots-entry
+    // table of region ids (kNone = empty; the previous batch's largest hot regions, each at
+    // one of its two hash slots, route_slots). A routed region's requests get bin
+    // lo_bins + slot, every other request its low digit; the upsweep stores each request's
+    // digit in `digit`, the scatter reads it back, and routed records go straight to
+    // rec_out_route (the final record array) at their pass-0 position, skipping pass 1.
+    const uint32_t* route_list;
+    uint32_t lo_bins;
+    void* rec_out_route;
+    uint16_t* digit;           // [n]: pass-0 digit per request (routing only)
+    const uint32_t* n_dev;     // pass 1: records to partition, on device (the normal ones)
 };
 
 struct HotInfo;
@@ -114,6 +129,14 @@ struct RegionArgs {
                                // claiming regions from `work` (0: one workgroup per region)
     uint64_t* dbg;             // nullable (rl_tune "debug_regions"): per bin kDbgWords words
                                // {t_start, t_end, records, rounds, 4 x cycle counters}
+    // nullable: dispatch order of the normal regions, largest size class first (block g runs
+    // region order[g]; order[n_regions] = number of non-empty regions listed)
+    const uint32_t* order;
+    uint32_t order_prefix;     // that many of the smallest regions are dispatched first
+    // routed hot regions (hot_list entries with kHotRoutedBit): region, first record, count
+    const uint32_t* route_list;
+    const uint32_t* route_start;
+    const uint32_t* route_cnt;
 };
 
 constexpr int kMaxShards = 64;              // routing: shards per router
@@ -125,11 +148,24 @@ struct DirSlot { uint64_t tag; uint32_t owner; uint32_t pad; };
 constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
 // hot_list layout: [kHotMax] list, then the selection's meta words: [0] listed count,
 // [1 .. 33] size-class histogram, [kHotClassCursor ..+33] per-class list cursors, then
-// [kHotTotalOff .. +2] chunk / group totals (k_hot_scan).
+// [kHotTotalOff .. +2] chunk / group totals (k_hot_scan), [kHotRoutedOff] routed entries
+// listed first (k_hot_route_list).
 constexpr uint32_t kHotClassCursor = 34;
-constexpr uint32_t kHotMetaWords = 68;   // zeroed before every batch
 constexpr uint32_t kHotTotalOff = 68;
+constexpr uint32_t kHotRoutedOff = 70;
+constexpr uint32_t kHotMetaWords = 71;   // zeroed before every batch
 constexpr uint32_t kHotListWords = kHotMax + 72;
+// A hot_list entry with this bit names route slot (entry & ~bit), not a normal bin.
+constexpr uint32_t kHotRoutedBit = 0x80000000u;
+// Hot-region routing: at most kRouteMax regions (the previous batch's largest hot regions)
+// get pass-0 bins of their own, one per slot of a kRouteSlots-entry table in which a region
+// sits at one of its two hash slots (route_slots): a lookup is two independent reads.
+constexpr uint32_t kRouteMax = 512;
+constexpr uint32_t kRouteSlots = 2048;
+__host__ __device__ inline void route_slots(uint32_t region, uint32_t& s1, uint32_t& s2) {
+    s1 = (region * 0x9E3779B1u) >> 21;
+    s2 = ((region ^ 0x5BD1E995u) * 0x85EBCA6Bu) >> 21;
+}
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
 constexpr uint32_t kDbgWords = 8;        // debug words per bin
 // Batch counters are sharded: one device-scope atomic word sustains only ~88 adds per us
@@ -264,6 +300,21 @@ hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, con
                              uint32_t* hot_count, uint32_t* hot_mark, uint32_t epoch,
                              hipStream_t s);
 hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s);
+// Routing: after the pass-0 scan, copy the routed bins' ranges (before pass 1 reuses the scan
+// arrays) and set ctl->n_normal; after the hot selection, list the routed regions first; after
+// the batch's hot preparation, the next batch's route list (largest listed regions >= thr).
+hipError_t launch_route_ranges(const uint32_t* bin_base, const uint32_t* bin_total, uint32_t lo_bins,
+                               uint32_t* route_start, uint32_t* route_cnt, BatchCtl* ctl, hipStream_t s);
+hipError_t launch_hot_route_list(const uint32_t* route_list, const uint32_t* route_cnt,
+                                 uint32_t* hot_list, uint32_t* hot_meta, hipStream_t s);
+// Normal-region dispatch order, largest power-of-two size class first (regions are
+// independent; a big region dispatched last would set the stage's tail). meta: kOrderMeta
+// words, zeroed by the launcher; order: [n_bins + 1].
+constexpr uint32_t kOrderMeta = 72;
+hipError_t launch_region_order(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
+                               uint32_t n_bins, uint32_t* meta, uint32_t* order, hipStream_t s);
+hipError_t launch_route_next(const HotInfo* hot_info, const uint32_t* hot_count, uint32_t threshold,
+                             uint32_t* route_list, hipStream_t s);
 hipError_t launch_unpermute(const UnpermArgs& a, int res_bytes, hipStream_t s);
 hipError_t launch_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok, uint32_t n,
                                hipStream_t s);

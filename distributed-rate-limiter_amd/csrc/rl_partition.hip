@@ -9,11 +9,16 @@ namespace rl {
 // ------------------------------------------------------------------ 1. upsweep
 template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
-    __shared__ uint32_t hist[1u << kMaxDigitBits];
+    // dynamic LDS (upsweep_lds_bytes): the histogram of this pass's bins, then the route table
+    // when routing; sized to the pass so that 4 workgroups fit a CU at 8192 bins
+    extern __shared__ uint32_t dyn_lds[];
     __shared__ LimLds L;
     const uint32_t t = threadIdx.x;
-    const uint32_t bins = 1u << a.digit_bits;
+    const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
+    uint32_t* hist = dyn_lds;
+    RouteLds& R = *(RouteLds*)(dyn_lds + bins);
     load_lim_lds(L, a);
+    if (a.route_list) route_load(R, a.route_list);
     if constexpr (RAW) {
         if (blockIdx.x == 0 && t == 0) {
             BatchCtl* c = a.ctl;
@@ -25,21 +30,27 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
             c->allowed = c->distinct = c->invalid = c->cap_err = c->regions = c->cache_hits = 0;
             c->grow[0] = c->grow[1] = c->grow[2] = c->grow[3] = 0;
             c->table_bytes = 0;
+            c->n_normal = a.n;                           // k_route_ranges lowers it when routing
         }
     }
-    const uint32_t mask = bins - 1;
+    // later passes partition the normal records only (their count is on device)
+    const uint32_t n = a.n_dev ? *a.n_dev : a.n;
     for (uint32_t it = 0;; ++it) {
         const uint32_t tile = tile_at(it, a.n_tiles);
         if (tile >= a.n_tiles) break;
         for (uint32_t b = t; b < bins; b += kTileThreads) hist[b] = 0;
         __syncthreads();
+        if (tile * (uint64_t)kTile < n) {
 #pragma unroll 8
-        for (int r = 0; r < kTileItems; ++r) {
-            const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
-            if (i < a.n) {
-                const uint32_t g = bin_of<Codec, RAW>(a, i, L);
-                atomicAdd(&hist[(g >> a.digit_shift) & mask], 1u);
-                if (a.region_count) atomicAdd(&a.region_count[g], 1u);
+            for (int r = 0; r < kTileItems; ++r) {
+                const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+                if (i < n) {
+                    const uint32_t g = bin_of<Codec, RAW>(a, i, L);
+                    const uint32_t d = pass_digit(a, g, R);
+                    atomicAdd(&hist[d], 1u);
+                    if (RAW && a.digit) a.digit[i] = (uint16_t)d;     // the scatter reads it back
+                    if (a.region_count) atomicAdd(&a.region_count[g], 1u);
+                }
             }
         }
         __syncthreads();
@@ -105,13 +116,14 @@ struct ScatterIn;
 
 template <class Codec>
 struct ScatterIn<Codec, true> {
-    uint64_t key; int64_t now_ns; int32_t permits; uint32_t lim; uint32_t op;
+    uint64_t key; int64_t now_ns; int32_t permits; uint32_t lim; uint32_t op; uint32_t dig;
     __device__ inline void load(const PartArgs& a, uint32_t i) {
         key = ld<kNtScIn>(a.key + i);
         now_ns = ld<kNtScIn>(a.now_ns + i);
         permits = ld<kNtScIn>(a.permits + i);
         lim = a.limiter ? a.limiter[i] : 0u;
         op = a.op ? a.op[i] : 0u;
+        dig = a.digit ? ld<kNtScIn>(a.digit + i) : 0u;
     }
 };
 
@@ -139,17 +151,21 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     __shared__ LimLds L;
     __shared__ uint64_t s_mm[2][kTileThreads / 64];
     const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    const uint32_t bins = 1u << a.digit_bits, mask = bins - 1;
+    const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
     load_lim_lds(L, a);
     int64_t base = 0;
     if constexpr (RAW) base = a.ctl->base_ms;
-    const uint32_t last = a.n - 1;
+    // later passes partition the normal records only (their count is on device); lanes past
+    // it store to the padding past the whole batch (a.n), clear of the routed records
+    const uint32_t n = a.n_dev ? *a.n_dev : a.n;
+    const uint32_t last = n - 1;
     uint64_t mn = ~0ULL, mx = 0;
     bool overflow = false;
     for (uint32_t it = 0;; ++it) {
         const uint32_t tile = tile_at(it, a.n_tiles);
         if (tile >= a.n_tiles) break;
         const uint32_t tile0 = tile * (uint32_t)kTile;
+        if (tile0 >= n) continue;                        // (workgroup-uniform)
         __syncthreads();     // previous tile's LDS users are done
         for (uint32_t b = t; b < bins; b += kTileThreads) {
             cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
@@ -163,7 +179,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
         __syncthreads();
         auto round = [&](const ScatterIn<Codec, RAW>& in, int r) {
             const uint32_t i = tile0 + (uint32_t)r * kTileThreads + t;
-            const bool active = i < a.n;
+            const bool active = i < n;
             Rec rec{};
             uint32_t d = 0;
             if (active) {
@@ -188,13 +204,15 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                         mn = k < mn ? k : mn;
                         mx = k > mx ? k : mx;
                     }
-                    d = (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
-                         >> a.digit_shift) & mask;
+                    // routing: the upsweep's digit (route-table lookup done once per request)
+                    d = a.digit ? (uint32_t)in.dig
+                                : (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                                   >> a.digit_shift) & ((1u << a.digit_bits) - 1);
                 } else {
                     rec = in.rec;
                     const uint32_t lim = Codec::limiter_of(rec);
                     d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
-                         >> a.digit_shift) & mask;
+                         >> a.digit_shift) & ((1u << a.digit_bits) - 1);
                 }
             }
             const uint32_t abl = a.ablate;
@@ -215,11 +233,13 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                 atomicAdd(&cur[d], cnt);
                 ((uint8_t*)&cntw[d])[wid] = 0;
             }
-            if (abl & (kAblNoMatch | kAblNoBarrier)) pos = min(pos, a.n - 1);
+            if (abl & (kAblNoMatch | kAblNoBarrier)) pos = min(pos, n - 1);
             // inactive lanes write to the padding slot past n (buffers carry spare entries)
             uint32_t wpos = active ? pos : a.n + t;
             if (abl & kAblSeqRecStore) wpos = active ? i : a.n + t;
-            if (!(abl & kAblNoRecStore)) st_rec<kNtScRec>((Rec*)a.rec_out + wpos, rec);
+            // a routed region's records go straight to the final record array
+            Rec* dst = (Rec*)(a.route_list && active && d >= a.lo_bins ? a.rec_out_route : a.rec_out);
+            if (!(abl & kAblNoRecStore)) st_rec<kNtScRec>(dst + wpos, rec);
             if (!(abl & kAblNoPosStore)) st<kNtScPos>(a.pos_out + (active ? i : a.n + t), pos);
         };
         // Unrolled by the prefetch depth so the input registers rotate without moves (a
@@ -301,6 +321,20 @@ __global__ __launch_bounds__(256) void k_bin_bounds(BoundsArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ routing helpers
+// After the pass-0 scan: the routed bins' ranges (pass 1 reuses bin_base / bin_total) and
+// the number of normal records, which pass 1 and the unpermute read on device.
+__global__ __launch_bounds__(1024) void k_route_ranges(const uint32_t* __restrict__ bin_base,
+                                                       const uint32_t* __restrict__ bin_total,
+                                                       uint32_t lo_bins, uint32_t* route_start,
+                                                       uint32_t* route_cnt, BatchCtl* ctl) {
+    for (uint32_t i = threadIdx.x; i < kRouteSlots; i += blockDim.x) {
+        route_start[i] = bin_base[lo_bins + i];
+        route_cnt[i] = bin_total[lo_bins + i];
+    }
+    if (threadIdx.x == 0) ctl->n_normal = bin_base[lo_bins];
+}
+
 // ------------------------------------------------------------------ 5. unpermute
 template <class Res>
 __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
@@ -360,8 +394,10 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
             p[k] = pos0[i < a.n ? i : 0];
         }
         if (pos1) {
+            // pass 1 moved the normal records only; routed ones kept their pass-0 position
+            const uint32_t nn = a.ctl->n_normal;
 #pragma unroll
-            for (int k = 0; k < B; ++k) p[k] = pos1[p[k]];
+            for (int k = 0; k < B; ++k) p[k] = p[k] < nn ? pos1[p[k]] : p[k];
         }
         if (a.ablate & kAblNoGather) {
 #pragma unroll
@@ -393,7 +429,7 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
         const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
         if (i >= a.n) break;
         uint32_t j = pos0[i];
-        if (a.pos1_final) j = a.pos1_final[j];
+        if (a.pos1_final && j < a.ctl->n_normal) j = a.pos1_final[j];
         if ((uint64_t)rf[j] == kResEscape) {
           allowed[i] = 0;
           remaining[i] = a.ext[j];
@@ -410,17 +446,20 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
 // whole result array. k_unpermute then gathers mid[pos0[i]] (2^d0 streams). Two
 // local gathers replace the composed res[pos1[pos0[i]]], which hit a random line of a
 // 1 GB index and of the result array per request.
+// Routed records (pass-0 positions >= ctl->n_normal) skipped pass 1: mid[j] = res[j].
 template <class Res>
 __global__ __launch_bounds__(256) void k_unpermute_mid(const uint32_t* __restrict__ pos1,
                                                        const Res* __restrict__ res,
-                                                       Res* __restrict__ mid, uint32_t n) {
+                                                       Res* __restrict__ mid, uint32_t n,
+                                                       const BatchCtl* __restrict__ ctl) {
     constexpr int B = 8;
     const uint32_t base = blockIdx.x * (256u * B) + threadIdx.x;
+    const uint32_t nn = ctl->n_normal;
     uint32_t p[B];
 #pragma unroll
     for (int k = 0; k < B; ++k) {
         const uint32_t j = base + (uint32_t)k * 256u;
-        p[k] = pos1[j < n ? j : 0];
+        p[k] = j < nn ? pos1[j] : j < n ? j : 0;
     }
     Res v[B];
 #pragma unroll
@@ -444,12 +483,15 @@ __global__ void k_fill_invalid(uint8_t* allowed, int64_t* remaining, double* tok
 
 hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
     dim3 grid(persistent_grid(a.n_tiles, a.up_per_cu ? a.up_per_cu : 4)), block(kTileThreads);
+    const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
+    if (bins > (1u << kMaxDigitBits)) return hipErrorInvalidValue;
+    const size_t lds = bins * sizeof(uint32_t) + (a.route_list ? sizeof(RouteLds) : 0);
     if (raw) {
-        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_upsweep<CodecC, true>), grid, block, 0, s, a);
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, true>), grid, block, lds, s, a);
     } else {
-        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, false>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_upsweep<CodecC, false>), grid, block, 0, s, a);
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, false>), grid, block, lds, s, a);
     }
     return hipGetLastError();
 }
@@ -527,7 +569,14 @@ hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s) {
 template <class Res>
 static void unpermute_mid(const UnpermArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_unpermute_mid<Res>, dim3((a.n + 2047) / 2048), dim3(256), 0, s, a.pos1,
-                       (const Res*)a.res, (Res*)a.mid, a.n);
+                       (const Res*)a.res, (Res*)a.mid, a.n, a.ctl);
+}
+
+hipError_t launch_route_ranges(const uint32_t* bin_base, const uint32_t* bin_total, uint32_t lo_bins,
+                               uint32_t* route_start, uint32_t* route_cnt, BatchCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(k_route_ranges, dim3(1), dim3(1024), 0, s, bin_base, bin_total, lo_bins,
+                       route_start, route_cnt, ctl);
+    return hipGetLastError();
 }
 
 hipError_t launch_unpermute(const UnpermArgs& a_in, int res_bytes, hipStream_t s) {

@@ -414,7 +414,17 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     constexpr uint32_t RPB = 1u << BS;              // regions per bin
 
     // RPB = 8: block g = 64q + 8r + x  ->  bin 8q + x, region r of that bin (see above)
-    const uint32_t bin = RPB == 1 ? g : (g / 64) * 8 + (g % 8);
+    uint32_t bin = RPB == 1 ? g : (g / 64) * 8 + (g % 8);
+    if (RPB == 1 && a.order) {
+        // largest regions first (k_order_place), after a prefix of the smallest: the first
+        // workgroups the machine takes then finish quickly and the hot chains (a side
+        // stream of higher priority) get their slots at once instead of behind the longest
+        // normal regions
+        const uint32_t tot = a.order[a.n_regions];
+        if (g >= tot) return;
+        const uint32_t k = min(a.order_prefix, tot);
+        bin = a.order[g < k ? tot - k + g : g - k];
+    }
     const uint32_t rb = RPB == 1 ? 0u : (g / 8) % 8;
     const uint32_t n_bins = a.n_regions / RPB;
     if (bin >= n_bins) return;

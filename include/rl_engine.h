@@ -219,7 +219,12 @@ int  rl_batch_stats_get(rl_engine* e, rl_batch_stats* out);
 int  rl_stage_times(rl_engine* e, const char** names, float* ms, int cap);
 int  rl_sync(rl_engine* e);
 /* Tuning / measurement knobs (not needed by callers): "ablate" = bit set of
- * measurement-only kernel variants whose results are NOT valid (0 = product path). */
+ * measurement-only kernel variants whose results are NOT valid (0 = product path);
+ * "hot_threshold" (records per region for the hot-key chains, 0 = off), "route" (two-pass
+ * tables: the previous batch's hot regions skip the second partition pass, default 1),
+ * "region_order" (largest regions dispatched first, default 1), "sparse_max", "split_hot",
+ * "region_walk", "bin_shift", "stage_timing", "debug_regions" and the "*_per_cu" grid
+ * sizes. Every setting gives the same decisions. */
 int  rl_tune(rl_engine* e, const char* key, int64_t value);
 /* Diagnostics (not needed by callers). "region_times": after a batch run with
  * rl_tune("debug_regions", 1), copies per-bin {t_start, t_end, records, rounds,

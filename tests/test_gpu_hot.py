@@ -139,3 +139,86 @@ def test_hot_stats_and_device_entry():
     assert s["allowed"] == int(want[0].sum())
     assert s["distinct_keys"] == len(np.unique(tr[0]))
     assert e.stage_times()["hot_fill"] > 0
+
+
+# ---- hot-region routing (two-pass tables): from the second batch on, the previous batch's
+# hot regions get pass-0 bins of their own, skip pass 1 and are read by the chains from
+# their pass-0 positions; the unpermute maps their results back without pass 1.
+def run_grow(limiters, tr, batches, grow_at, **kw):
+    """run() with an explicit rl_grow_limiter before batch `grow_at` (region ids change, so
+    the route list is dropped)."""
+    kw.setdefault("max_batch", 1 << 22)
+    e = rl_amd.Engine(**kw)
+    for l in limiters:
+        e.add_limiter(*l)
+    o = COracle(limiters)
+    n = len(tr[0])
+    cuts = np.linspace(0, n, batches + 1).astype(int)
+    got = [[], [], []]
+    for b in range(batches):
+        if b == grow_at:
+            for li in range(len(limiters)):
+                e.grow_limiter(li, 2 * e.limiter_slots(li))
+        sl = slice(cuts[b], cuts[b + 1])
+        a, r, t, st = e.execute(*(x[sl] for x in tr))
+        assert st in (rl_amd.RL_OK, rl_amd.RL_E_INVALID_REQUEST), rl_amd.strerror(st)
+        got[0].append(a); got[1].append(r); got[2].append(t)
+    return tuple(np.concatenate(g) for g in got), o.run(*tr), e
+
+
+@pytest.mark.parametrize("algo", ["sw", "tb"])
+@pytest.mark.parametrize("route", [1, 0])
+def test_hot_routed_two_pass(algo, route):
+    # hot keys at their limits over 5 batches of a two-pass table, with peeks / resets /
+    # invalid requests; routing on and off give the oracle's results (tokens bit-exact)
+    lims = ([[rl_amd.SW, 200, 20_000, 0.0], [rl_amd.SW, 5, 1000, 0.0]] if algo == "sw" else
+            [[rl_amd.TB, 50, 60_000, 10.0], [rl_amd.TB, 20, 5_000, 3.0]])
+    tr = hot_trace(31, 2_000_000, 300_000, 0.5, [0, 1], 100_000, ops=0.005, hot_keys=6)
+    tr[1][::997] = 0                                     # invalid (permits 0)
+    got, want, _ = run(lims, tr, batches=5, capacity=1 << 22,
+                       tune={"hot_threshold": 8192, "route": route})
+    assert_same(got, want, f"routed {algo} route={route}")
+
+
+def test_hot_routed_shifting_hot_set():
+    # the hot keys change every batch: regions routed because of the previous batch are
+    # small (or empty) in this one and still go through the chains
+    lims = [[rl_amd.SW, 100, 10_000, 0.0], [rl_amd.TB, 30, 20_000, 5.0]]
+    parts = [hot_trace(40 + b, 400_000, 200_000, 0.6, [0, 1], 20_000, hot_keys=5) for b in range(4)]
+    off = np.int64(0)
+    cols = [[], [], [], [], []]
+    for b, p in enumerate(parts):
+        for c in range(5):
+            x = p[c]
+            if c == 2:
+                x = x + np.int64(b) * 20_000 * NS        # consecutive time slices
+            cols[c].append(x)
+    tr = tuple(np.concatenate(c) for c in cols)
+    got, want, _ = run(lims, tr, batches=4, capacity=1 << 22, tune={"hot_threshold": 4096})
+    assert_same(got, want, "routed shifting")
+
+
+def test_hot_routed_every_region():
+    # hot_threshold 1 on a two-pass table: the 1024 largest regions of every batch are listed
+    # and routed in the next (routed regions of every size, many with one or two records)
+    lims = [[rl_amd.SW, 50, 30_000, 0.0], [rl_amd.TB, 40, 30_000, 8.0]]
+    tr = trace(33, 1_200_000, 400_000, 2, 150_000, zipf=1.2, ops=0.02, invalid=0.001)
+    got, want, _ = run(lims, tr, batches=4, capacity=1 << 22, tune={"hot_threshold": 1})
+    assert_same(got, want, "routed every region")
+
+
+def test_hot_routed_growth_clears_routes():
+    # growth renumbers regions: the route list of the batch before is dropped, not misapplied
+    lims = [[rl_amd.SW, 300, 60_000, 0.0], [rl_amd.TB, 50, 60_000, 10.0]]
+    tr = hot_trace(34, 1_500_000, 200_000, 0.4, [0, 1], 90_000, hot_keys=4)
+    got, want, e = run_grow(lims, tr, batches=4, grow_at=2, capacity=1 << 22)
+    assert_same(got, want, "routed growth")
+
+
+@pytest.mark.parametrize("order", [1, 0])
+def test_region_order_knob(order):
+    # largest-first region dispatch (default) and identity order give the oracle's results
+    lims = [[rl_amd.SW, 20, 10_000, 0.0], [rl_amd.TB, 30, 20_000, 5.0]]
+    tr = trace(35, 800_000, 60_000, 2, 60_000, zipf=1.15, ops=0.01)
+    got, want, _ = run(lims, tr, batches=3, capacity=1 << 16, tune={"region_order": order})
+    assert_same(got, want, f"region_order={order}")
