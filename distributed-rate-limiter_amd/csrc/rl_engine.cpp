@@ -104,7 +104,7 @@ struct rl_engine {
     // hot regions
     uint32_t* hot_list = nullptr;           // [kHotListWords]: list, k_hot_select's meta, totals
     HotInfo* hot_info = nullptr;            // [kHotMax]
-    uint64_t* hot_summ = nullptr;           // [hot_summ_cap][4]
+    uint64_t* hot_summ = nullptr;           // [hot_summ_cap][8]
     size_t hot_summ_cap = 0, hot_summ_l1 = 0;
     uint32_t* hot_mark = nullptr;           // [hot_mark_cap] epoch marks per bin
     size_t hot_mark_cap = 0;
@@ -527,13 +527,13 @@ static int ensure_regions(BatchScratch& B, size_t bins) {
     return RL_OK;
 }
 
-// chunk summaries [l1] then group summaries [l1 / 64 + kHotMax + 1], 32 B each
+// chunk summaries [l1] then group summaries [l1 / 64 + kHotMax + 1], 64 B each (two keys)
 static int ensure_hot_summ(rl_engine* e, size_t n) {
     const size_t l1 = n / kHotChunk + kHotMax + 1;
     const size_t need = l1 + l1 / 64 + kHotMax + 1;
     if (need <= e->hot_summ_cap) return RL_OK;
     dfree(e->hot_summ);
-    if (dalloc(&e->hot_summ, need * 4) != RL_OK) { e->hot_summ_cap = 0; return RL_E_NOMEM; }
+    if (dalloc(&e->hot_summ, need * 8) != RL_OK) { e->hot_summ_cap = 0; return RL_E_NOMEM; }
     e->hot_summ_cap = need;
     e->hot_summ_l1 = l1;
     return RL_OK;
@@ -738,7 +738,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ra.hot_list = e->hot_list; ra.hot_count = hot_count; ra.hot_mark = e->hot_mark;
         ra.epoch = e->epoch;
         ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ;
-        ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 4; ra.hot_total = e->hot_list + kHotMax + kHotTotalOff;
+        ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 8; ra.hot_total = e->hot_list + kHotMax + kHotTotalOff;
         ra.route_list = e->route_list; ra.route_start = e->route_start; ra.route_cnt = e->route_cnt;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
         // the next batch's routed regions: this batch's largest hot regions (two-pass tables)

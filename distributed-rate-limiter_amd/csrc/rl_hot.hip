@@ -23,46 +23,6 @@ __global__ __launch_bounds__(1024) void k_hot_scan(RegionArgs a) {
     if (t == 0) { a.hot_total[0] = tot; a.hot_total[1] = tot2; }
 }
 
-// Phase A2 (one wave per 64 chunks): the same summary over 4096 records, so the chain
-// decides the long runs of a hot key's denials 4096 records per test.
-__global__ __launch_bounds__(256) void k_hot_summ2(RegionArgs a) {
-    __shared__ uint32_t s_base[kHotMax + 1];
-    const uint32_t hc = min(a.hot_count[0], kHotMax);
-    const uint32_t total = a.hot_total[1];
-    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].group_base;
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t g = blockIdx.x * 4 + wid; g < total; g += gridDim.x * 4) {
-        const uint32_t i = hot_region_of(s_base, hc, g);
-        const HotInfo f = a.hot_info[i];
-        const uint32_t c = (g - s_base[i]) * 64 + lane;
-        uint64_t mn = ~0ULL, mx = 0;
-        uint32_t w = 0;
-        if (c < f.n_chunks) {
-            const uint64_t* d = a.hot_summ + (size_t)(f.chunk_base + c) * 4;
-            mn = ord_key((int64_t)d[0]);
-            mx = ord_key((int64_t)d[1]);
-            w = (uint32_t)d[2];
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t x = __shfl_xor(mn, o, 64), y = __shfl_xor(mx, o, 64);
-            mn = x < mn ? x : mn;
-            mx = y > mx ? y : mx;
-        }
-        const uint32_t ns = __ballot((w & 0xFFu) != 0) ? 1u : 0u;       // flags, not counts
-        const uint32_t nh = __ballot(((w >> 8) & 0xFFu) != 0) ? 1u : 0u;
-        const uint32_t ne = __ballot(((w >> 16) & 0xFFu) != 0) ? 1u : 0u;
-        const uint32_t no = __ballot(((w >> 24) & 0xFFu) != 0) ? 1u : 0u;
-        if (lane == 0) {
-            uint64_t* d = a.hot_summ2 + (size_t)g * 4;
-            d[0] = mn ^ 0x8000000000000000ULL;
-            d[1] = mx ^ 0x8000000000000000ULL;
-            d[2] = ns | (nh << 8) | (ne << 16);
-            d[3] = (uint64_t)no << 8;                   // other keys: kept through the verdict
-        }
-    }
-}
-
 // Hot-region selection, largest first: k_hot_hist counts the bins at or above the
 // threshold per power-of-two size class; k_hot_select then raises the threshold to the
 // smallest class boundary that admits at most kHotMax bins and lists those bins.
@@ -270,7 +230,6 @@ hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s) {
     hipLaunchKernelGGL(k_hot_scan, dim3(1), dim3(1024), 0, s, a);
     if (wide) hipLaunchKernelGGL(k_hot_summ<CodecW>, gp, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_hot_summ<CodecC>, gp, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_hot_summ2, gp, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -154,7 +154,10 @@ __device__ inline uint32_t hot_region_of(const uint32_t* s_base, uint32_t hc, ui
 }
 
 // Phase 0 (one wave per listed region): bounds, chunks and the dominant key of a sample
-// of the region's first 64 records (a hot region is dominated by its hot key).
+// of the region's first 64 records (a hot region is dominated by its hot key), and a
+// second key when the sample says it holds >= kHot2MinRecords of the region.
+constexpr uint32_t kHot2MinSample = 4;
+constexpr uint32_t kHot2MinRecords = 32768;
 template <class Codec>
 __global__ __launch_bounds__(64) void k_hot_prep(RegionArgs a) {
     const uint32_t hc = min(a.hot_count[0], kHotMax);
@@ -188,72 +191,132 @@ __global__ __launch_bounds__(64) void k_hot_prep(RegionArgs a) {
     uint32_t key = (act && ok) ? (cnt << 6) | (63u - lane) : 0u;
     for (int o = 32; o > 0; o >>= 1) key = max(key, (uint32_t)__shfl_xor((int)key, o, 64));
     const uint64_t tag = __shfl(h, (int)(63u - (key & 63u)), 64);
+    // a second heavy key (two hot Zipf keys in one region): its own chain, or wave 1 would
+    // apply its ~10^5 records 64 at a time (sw_zipf: a 398K-record region set the stage)
+    uint32_t key2 = (act && ok && h != tag) ? (cnt << 6) | (63u - lane) : 0u;
+    for (int o = 32; o > 0; o >>= 1) key2 = max(key2, (uint32_t)__shfl_xor((int)key2, o, 64));
+    const uint64_t tag2 = __shfl(h, (int)(63u - (key2 & 63u)), 64);
+    const uint32_t c1 = key >> 6, c2 = key2 >> 6;
+    const bool two = c1 >= 2u && c2 >= kHot2MinSample &&
+                     (uint64_t)(end - start) * c2 >= (uint64_t)kHot2MinRecords * n0;
     if (lane == 0) {
         HotInfo f;
         f.tag = tag; f.bin = bin; f.start = start; f.end = end;
         f.n_chunks = (end - start + kHotChunk - 1) / kHotChunk;
         f.chunk_base = 0;
-        f.ok = (key >> 6) >= 2u ? 1u : 0u;
+        f.ok = (c1 >= 2u ? 1u : 0u) | (two ? 2u : 0u);
         f.n_groups = (f.n_chunks + 63) / 64;
         f.group_base = 0;
-        f.pad[0] = f.pad[1] = 0;
+        f.tag2 = two ? tag2 : 0;
         a.hot_info[i] = f;
     }
 }
 
 
 
-// Phase A (one wave per 64-record chunk, all CUs): what the chain needs to decide the hot
-// key's records of a chunk without reading it: the time range of its plain acquires, and
-// how many of its records need the exact path (peek / reset). Summary words: [0] min now,
-// [1] max now, [2] n_special | n_hot << 8 | n_early << 16 | n_other << 24, [3] verdict:
-// bit 0 = hot records decided by the thresholds (words 0-2 then hold the key's state),
-// bit 1 = TB early rejects among them, bits 8-15 = records of other keys.
+// Phase A (one wave per group of 64 chunks, all CUs): what a chain needs to decide its key's
+// records of a chunk (64 records) or a group (4096) without reading them: the time range of
+// its plain acquires, and how many of its records need the exact path (peek / reset). Eight
+// words per chunk, four per key (key k at 4k): [0] min now, [1] max now, [2] n_special |
+// n_hot << 8 | n_early << 16 | n_rest << 24, [3] verdict: bit 0 = the key's records decided
+// by the thresholds (words 0-2 then hold its state), bit 1 = TB early rejects among them,
+// bits 8-15 = n_rest. n_rest counts the records of other keys: for the dominant key every
+// other record, for the second key those of neither (the records wave 1 applies). Group
+// words: the same over the group's chunks, with 0/1 flags for the counts. The wave keeps
+// four chunks' records in flight.
+__device__ inline uint64_t wave_min64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) { const uint64_t x = __shfl_xor(v, o, 64); v = x < v ? x : v; }
+    return v;
+}
+__device__ inline uint64_t wave_max64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) { const uint64_t x = __shfl_xor(v, o, 64); v = x > v ? x : v; }
+    return v;
+}
+
 template <class Codec>
 __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
+    using Rec = typename Codec::Rec;
     __shared__ uint32_t s_base[kHotMax + 1];
     const uint32_t hc = min(a.hot_count[0], kHotMax);
-    const uint32_t total = a.hot_total[0];
-    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].chunk_base;
+    const uint32_t total = a.hot_total[1];
+    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].group_base;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
+    const Rec* recs = (const Rec*)a.rec;
     const int64_t base = a.ctl->base_ms;
-    for (uint32_t g = blockIdx.x * 4 + wid; g < total; g += gridDim.x * 4) {
-        const uint32_t i = hot_region_of(s_base, hc, g);
+    for (uint32_t gg = blockIdx.x * 4 + wid; gg < total; gg += gridDim.x * 4) {
+        const uint32_t i = hot_region_of(s_base, hc, gg);
         const HotInfo f = a.hot_info[i];
         const DevLimiter& L = a.lims[a.region_lim[f.bin]];
-        const uint32_t j = f.start + (g - s_base[i]) * kHotChunk + lane;
-        const bool valid = j < f.end;
-        Req q{};
-        if (valid) q = Codec::dec(recs[j], base);
-        const bool hot = valid && f.ok && !q.invalid && q.h == f.tag;
-        const bool acq = q.op == (uint32_t)kOpAcquire;
-        const bool early = hot && acq && L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
-        const bool plain = hot && acq && !early;
-        const bool special = hot && !acq;                 // the hot key's peek / reset
-        const bool other = valid && !hot;                 // every other key (and invalid)
-        uint64_t mn = plain ? ord_key(q.now_ms) : ~0ULL, mx = plain ? ord_key(q.now_ms) : 0ULL;
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t x = __shfl_xor(mn, o, 64), y = __shfl_xor(mx, o, 64);
-            mn = x < mn ? x : mn;
-            mx = y > mx ? y : mx;
+        const bool tb = L.algo == kAlgoTB;
+        const int64_t maxp = L.max_permits;
+        const bool two = (f.ok & 2u) != 0;
+        const uint32_t c0 = (gg - s_base[i]) * 64, c1 = min(c0 + 64, f.n_chunks);
+        uint64_t gmn[2] = {~0ULL, ~0ULL}, gmx[2] = {0ULL, 0ULL};
+        uint32_t gfl[2] = {0u, 0u};                      // flags: special, hot, early, rest
+        auto load = [&](uint32_t c) { return recs[min(f.start + c * kHotChunk + lane, f.end - 1)]; };
+        auto chunk = [&](const Rec& r, uint32_t c) {
+            const uint32_t j = f.start + c * kHotChunk + lane;
+            const bool valid = j < f.end;
+            const Req q = Codec::dec(r, base);
+            const bool acq = q.op == (uint32_t)kOpAcquire;
+            const bool hot0 = valid && (f.ok & 1u) && !q.invalid && q.h == f.tag;
+            const bool hot1 = two && valid && !q.invalid && q.h == f.tag2;
+            uint64_t w[8];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const bool hot = k ? hot1 : hot0;
+                const bool early = hot && acq && tb && (int64_t)q.permits > maxp;
+                const bool plain = hot && acq && !early;
+                const bool special = hot && !acq;         // the key's peek / reset
+                // n_rest: not the dominant key / neither key (invalid records included)
+                const bool rest = valid && !hot0 && (k == 0 || !hot1);
+                uint64_t mn = ~0ULL, mx = 0ULL;
+                if (k == 0 || two) {                      // (wave-uniform)
+                    mn = wave_min64(plain ? ord_key(q.now_ms) : ~0ULL);
+                    mx = wave_max64(plain ? ord_key(q.now_ms) : 0ULL);
+                }
+                const uint32_t ns = (uint32_t)__popcll(__ballot(special));
+                const uint32_t nh = (uint32_t)__popcll(__ballot(hot));
+                const uint32_t ne = (uint32_t)__popcll(__ballot(early));
+                const uint32_t no = (uint32_t)__popcll(__ballot(rest));
+                w[4 * k + 0] = mn == ~0ULL ? (uint64_t)INT64_MAX : (mn ^ 0x8000000000000000ULL);
+                w[4 * k + 1] = mx == 0ULL ? (uint64_t)INT64_MIN : (mx ^ 0x8000000000000000ULL);
+                w[4 * k + 2] = ns | (nh << 8) | (ne << 16) | (no << 24);
+                w[4 * k + 3] = (uint64_t)no << 8;
+                gmn[k] = mn < gmn[k] ? mn : gmn[k];
+                gmx[k] = mx > gmx[k] ? mx : gmx[k];
+                gfl[k] |= (ns ? 1u : 0u) | (nh ? 2u : 0u) | (ne ? 4u : 0u) | (no ? 8u : 0u);
+            }
+            uint64_t v = w[0];                            // lanes 0-7: one 64-B store
+#pragma unroll
+            for (int k = 1; k < 8; ++k) v = lane == (uint32_t)k ? w[k] : v;
+            if (lane < 8) a.hot_summ[(size_t)(f.chunk_base + c) * 8 + lane] = v;
+        };
+        Rec q0 = load(c0), q1 = load(c0 + 1), q2 = load(c0 + 2), q3 = load(c0 + 3);
+        for (uint32_t c = c0; c < c1; c += 4) {
+            chunk(q0, c);     q0 = load(c + 4);
+            if (c + 1 >= c1) break;
+            chunk(q1, c + 1); q1 = load(c + 5);
+            if (c + 2 >= c1) break;
+            chunk(q2, c + 2); q2 = load(c + 6);
+            if (c + 3 >= c1) break;
+            chunk(q3, c + 3); q3 = load(c + 7);
         }
-        const uint32_t ns = (uint32_t)__popcll(__ballot(special));
-        const uint32_t nh = (uint32_t)__popcll(__ballot(hot));
-        const uint32_t ne = (uint32_t)__popcll(__ballot(early));
-        const uint32_t no = (uint32_t)__popcll(__ballot(other));
-        if (lane == 0) {
-            uint64_t* d = a.hot_summ + (size_t)g * 4;
-            d[0] = mn == ~0ULL ? (uint64_t)INT64_MAX : (mn ^ 0x8000000000000000ULL);
-            d[1] = mx == 0ULL ? (uint64_t)INT64_MIN : (mx ^ 0x8000000000000000ULL);
-            d[2] = ns | (nh << 8) | (ne << 16) | (no << 24);
-            d[3] = (uint64_t)no << 8;
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint64_t gw0 = gmn[k] ^ 0x8000000000000000ULL, gw1 = gmx[k] ^ 0x8000000000000000ULL;
+            const uint64_t gw2 = (gfl[k] & 1u) | ((gfl[k] >> 1 & 1u) << 8) | ((gfl[k] >> 2 & 1u) << 16);
+            const uint64_t gw3 = (uint64_t)(gfl[k] >> 3 & 1u) << 8;   // rest: kept through the verdict
+            v = lane == 4u * k ? gw0 : lane == 4u * k + 1 ? gw1 : lane == 4u * k + 2 ? gw2 :
+                lane == 4u * k + 3 ? gw3 : v;
         }
+        if (lane < 8) a.hot_summ2[(size_t)gg * 8 + lane] = v;
     }
 }
 
-// Phase B (one 2-wave workgroup per listed region, beside k_regions). Wave 0 (pass 1)
+// Phase B (one 3-wave workgroup per listed region, beside k_regions). Wave 0 (pass 1)
 // walks the region's summaries in arrival order with the hot key's threshold pair: a
 // group of 64 chunks, or a chunk, whose hot-key times all lie in [T0, T1) has its hot
 // records decided without being read (verdict + the key's state go back into the summary
@@ -261,14 +324,14 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
 // then the wavefront-per-key sequential run). Wave 1 (pass 2), at the same time, applies
 // every other key of the region in arrival order, 64 records at a time through
 // wave_apply. The passes touch disjoint slots of the shared LDS table (wave 0 only the
-// hot key's state, wave 1 never that slot), so they need no synchronisation.
-// Runs as the first kHotMax workgroups of k_regions<..., HOT = true>, so the chains are
-// dispatched before the normal regions fill the machine.
+// hot key's state, wave 1 never that slot), so they need no synchronisation. Wave 2 runs
+// pass 1 for a second dominant key when the region holds one (HotInfo::ok bit 1); wave 1
+// then applies the records of neither key.
 template <class Codec, class Res, bool TOK>
 __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Codec, true>& S) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
-    __shared__ int32_t s_hslot;
+    __shared__ int32_t s_hslot[2];
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (i >= hc) return;
@@ -284,7 +347,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     Res* res = (Res*)a.res;
     const uint32_t pad = a.n_total + lane;
     if (a.ctl->span_overflow != 0) {                  // whole batch rejected (see k_regions)
-        for (uint32_t j = f.start + threadIdx.x; j < f.end; j += 128) {
+        for (uint32_t j = f.start + threadIdx.x; j < f.end; j += blockDim.x) {
             res[j] = (Res)pack_result(false, kRemInvalid);
             if (TOK) a.tok[j] = __builtin_nan("");
         }
@@ -311,41 +374,56 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             }
         }
         wave_fence();
-        int32_t hslot = -1;
-        if (f.ok) {
-            const uint32_t p0 = slot_home(f.tag);
-            for (uint32_t k = 0; k < NS; ++k) {             // linear probing, as the rebuild
-                const uint32_t p = (p0 + k) & (NS - 1);
+        int32_t hsl[2] = {-1, -1};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (!((f.ok >> k) & 1u)) continue;              // (wave-uniform)
+            const uint64_t tg = k ? f.tag2 : f.tag;
+            const uint32_t p0 = slot_home(tg);
+            int32_t hslot = -1;
+            for (uint32_t m = 0; m < NS; ++m) {             // linear probing, as the rebuild
+                const uint32_t p = (p0 + m) & (NS - 1);
                 const uint32_t o = S.occ[p];
-                if (!(o & 1u) || S.tag[p] == f.tag) { hslot = (int32_t)p; break; }
+                if (!(o & 1u) || S.tag[p] == tg) { hslot = (int32_t)p; break; }
             }
             if (hslot >= 0 && !(S.occ[hslot] & 1u) && lane == 0) {
-                S.occ[hslot] = 1u; S.tag[hslot] = f.tag; S.sa[hslot] = 0; S.sb[hslot] = 0; S.sc[hslot] = 0;
+                S.occ[hslot] = 1u; S.tag[hslot] = tg; S.sa[hslot] = 0; S.sb[hslot] = 0; S.sc[hslot] = 0;
             }
+            wave_fence();
+            hsl[k] = hslot;
         }
-        if (lane == 0) s_hslot = hslot;
+        if (lane == 0) { s_hslot[0] = hsl[0]; s_hslot[1] = hsl[1]; }
     }
     __syncthreads();
-    // hot_ok false (no dominant key, or its region is full): pass 2 takes every record
-    const int32_t hslot = s_hslot;
-    const bool hot_ok = hslot >= 0;
-    const uint32_t hs = hot_ok ? (uint32_t)hslot : 0u;
-    const uint64_t tag = f.tag;
-    auto is_hot = [&](const Req& q, bool valid) { return hot_ok && valid && !q.invalid && q.h == tag; };
+    // hot_ok false (no dominant key, or its region is full): pass 2 takes every record; the
+    // second key has a chain only beside the first's
+    const int32_t hsl0 = s_hslot[0];
+    const int32_t hsl1 = hsl0 >= 0 ? s_hslot[1] : -1;
+    const bool hot_ok = hsl0 >= 0, hot_ok2 = hsl1 >= 0;
+    auto is_hot = [&](const Req& q, bool valid) {
+        return valid && !q.invalid && ((hot_ok && q.h == f.tag) || (hot_ok2 && q.h == f.tag2));
+    };
+    // summary words of chunk c / group g (8 per entry: 4 per key)
     auto summ_at = [&](uint32_t c) {
-        return a.hot_summ + (size_t)(f.chunk_base + (c < f.n_chunks ? c : 0)) * 4;
+        return a.hot_summ + (size_t)(f.chunk_base + (c < f.n_chunks ? c : 0)) * 8;
     };
     auto grp_at = [&](uint32_t g) {
-        return a.hot_summ2 + (size_t)(f.group_base + (g < f.n_groups ? g : 0)) * 4;
+        return a.hot_summ2 + (size_t)(f.group_base + (g < f.n_groups ? g : 0)) * 8;
     };
+    // the verdict word holding wave 1's "records of neither key" count in bits 8-15
+    const uint32_t rest_w = hot_ok2 ? 7u : 3u;
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0, n_other = 0;
     uint32_t n_changed = 0, n_tk = 0, n_fb = 0;       // debug: changes, [T0, T1) updates,
     uint32_t n_late = 0;                              // detailed chunks starting before T0 / ending past T1
     uint64_t cyc_run = 0, cyc_search = 0, cyc_detail = 0, cyc_pass2 = 0;   // debug stamps
     bool any_hot = false;
-    auto pass1 = [&](auto algo) {
+    auto pass1 = [&](auto algo, const uint32_t kk) {
         constexpr int A = decltype(algo)::value;
+        const uint32_t ow = 4u * kk;                      // this key's summary words
+        const uint32_t hs = (uint32_t)(kk ? hsl1 : hsl0);
+        const uint64_t tag = kk ? f.tag2 : f.tag;
+        auto is_key = [&](const Req& q, bool valid) { return valid && !q.invalid && q.h == tag; };
         // the hot key's state (registers; written to LDS when it changes) and the range
         // [T0, T1) in which every acquire is denied with remaining 0 (whole chunks and groups
         // inside it are decided without being read)
@@ -375,7 +453,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             pre_c = c + 1;
             pre = recs[min(f.start + pre_c * kHotChunk + lane, f.end - 1)];
             const Req q = Codec::dec(r, base);
-            const bool hot = is_hot(q, valid);
+            const bool hot = is_key(q, valid);
             bool oa = false;
             int64_t orem = 0;
             double tk = __builtin_nan("");
@@ -558,7 +636,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         auto walk_group = [&](uint32_t grp) {
             const uint32_t c = grp * 64 + lane;
             const bool has = c < f.n_chunks;
-            uint64_t* sm = summ_at(c);
+            uint64_t* sm = summ_at(c) + ow;
             const ulonglong2 v01 = *(const ulonglong2*)sm;
             const uint64_t v2 = sm[2];
             int64_t mn = INT64_MAX, mx = INT64_MIN;
@@ -593,17 +671,17 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             }
         };
         // level 2: 64 groups per test, the next 64 in flight
-        ulonglong2 nx01 = *(const ulonglong2*)grp_at(lane);
-        uint64_t nx2 = grp_at(lane)[2], nx3 = grp_at(lane)[3];
+        ulonglong2 nx01 = *(const ulonglong2*)(grp_at(lane) + ow);
+        uint64_t nx2 = grp_at(lane)[ow + 2], nx3 = grp_at(lane)[ow + 3];
         for (uint32_t g0 = 0; g0 < f.n_groups; g0 += 64) {
             const uint32_t g = g0 + lane;
             const bool has = g < f.n_groups;
-            uint64_t* sg = grp_at(g);
+            uint64_t* sg = grp_at(g) + ow;
             const ulonglong2 v01 = nx01;
             const uint64_t v2 = nx2, v3 = nx3;
-            nx01 = *(const ulonglong2*)grp_at(g + 64);
-            nx2 = grp_at(g + 64)[2];
-            nx3 = grp_at(g + 64)[3];
+            nx01 = *(const ulonglong2*)(grp_at(g + 64) + ow);
+            nx2 = grp_at(g + 64)[ow + 2];
+            nx3 = grp_at(g + 64)[ow + 3];
             const int64_t mn = (int64_t)v01.x, mx = (int64_t)v01.y;
             const uint32_t w = (uint32_t)v2;
             const bool ns = (w & 0xFFu) != 0, nh = ((w >> 8) & 0xFFu) != 0, ne = ((w >> 16) & 0xFFu) != 0;
@@ -667,7 +745,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         bool cdone = f.n_groups == 0;
         auto group_mask = [&](uint32_t g0) {
             const uint32_t g = g0 + lane;
-            return __ballot(g < f.n_groups && (!hot_ok || ((grp_at(g)[3] >> 8) & 1u)));
+            return __ballot(g < f.n_groups && (!hot_ok || ((grp_at(g)[rest_w] >> 8) & 1u)));
         };
         if (!cdone) cgtodo = group_mask(0);
         auto next_chunk = [&]() -> uint32_t {
@@ -682,7 +760,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 cgtodo &= cgtodo - 1;
                 const uint32_t c = cgrp * 64 + lane;
                 uint32_t no = 0;
-                if (c < f.n_chunks) no = hot_ok ? (uint32_t)(summ_at(c)[3] >> 8) & 0xFFu : 64u;
+                if (c < f.n_chunks) no = hot_ok ? (uint32_t)(summ_at(c)[rest_w] >> 8) & 0xFFu : 64u;
                 ctodo = __ballot(no != 0);
             }
             if (cdone) return kNone;
@@ -711,10 +789,11 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         if (count > 0) apply64(count);
         if (a.dbg) cyc_pass2 += __builtin_amdgcn_s_memtime() - c_p2;
     };
-    if (wid == 0) {
-        if (hot_ok) {
-            if (L.algo == kAlgoTB) pass1(std::integral_constant<int, kAlgoTB>{});
-            else pass1(std::integral_constant<int, kAlgoSW>{});
+    if (wid == 0 || wid == 2) {
+        const uint32_t kk = wid >> 1;
+        if (kk ? hot_ok2 : hot_ok) {
+            if (L.algo == kAlgoTB) pass1(std::integral_constant<int, kAlgoTB>{}, kk);
+            else pass1(std::integral_constant<int, kAlgoSW>{}, kk);
         }
     } else {
         if (L.algo == kAlgoTB) pass2(std::integral_constant<int, kAlgoTB>{});
@@ -734,9 +813,11 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     // ---- write the region back, statistics
     __shared__ uint64_t s_w1[2];                      // wave 1's debug counters
     if (wid == 1 && lane == 0) { s_w1[0] = n_other; s_w1[1] = cyc_pass2; }
-    const bool touched_hot = __syncthreads_or(any_hot);
+    const bool touched0 = __syncthreads_or(wid == 0 && any_hot);
+    const bool touched1 = __syncthreads_or(wid == 2 && any_hot);
     if (wid != 0) return;
-    if (lane == 0 && hot_ok && touched_hot) S.occ[hs] |= 2u;
+    if (lane == 0 && hot_ok && touched0) S.occ[hsl0] |= 2u;
+    if (lane == 0 && hot_ok2 && touched1) S.occ[hsl1] |= 2u;
     wave_fence();
     uint32_t touched = 0, used = 0;
     for (uint32_t sl = lane; sl < NS; sl += 64) {
@@ -768,81 +849,95 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     }
 }
 
-// One launch for both (rl_tune split_hot = 0): 2-wave workgroups; the first kHotMax run the
-// hot regions' chains, the rest two normal regions each, so the chains are dispatched before
-// the normal regions fill the machine, at the LDS per wave of the plain kernel.
+// One launch for both (rl_tune split_hot = 0): 3-wave workgroups; the first kHotMax run the
+// hot regions' chains, the rest three normal regions each, so the chains are dispatched
+// before the normal regions fill the machine, at the LDS per wave of the plain kernel.
 template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(128, RL_HOT_MIN_WAVES) void k_regions_hot(RegionArgs a) {
-    __shared__ union U { RegionTable two[2]; RegionLds<Codec, true> one; } S;
+__global__ __launch_bounds__(192, RL_HOT_MIN_WAVES) void k_regions_hot(RegionArgs a) {
+    __shared__ union U { RegionTable three[3]; RegionLds<Codec, true> one; } S;
     if (blockIdx.x < kHotMax) {
         hot_chain<Codec, Res, TOK>(a, blockIdx.x, S.one);
         return;
     }
-    region_body_t<Codec, Res, TOK, 0>(a, (blockIdx.x - kHotMax) * 2 + (threadIdx.x >> 6),
-                                      S.two[threadIdx.x >> 6]);
+    region_body_t<Codec, Res, TOK, 0>(a, (blockIdx.x - kHotMax) * 3 + (threadIdx.x >> 6),
+                                      S.three[threadIdx.x >> 6]);
 }
 
-// The hot chains alone (2-wave workgroups), launched on a side stream just before the
-// normal regions' single-wave launch: no normal region waits for the other region of a
-// 2-wave workgroup, and the chains still start first.
+// The hot chains alone (3-wave workgroups), launched on a side stream just before the
+// normal regions' single-wave launch: no normal region waits for another region of a
+// multi-wave workgroup, and the chains still start first.
 template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(128, RL_HOT_MIN_WAVES) void k_hot_chains(RegionArgs a) {
+__global__ __launch_bounds__(192, RL_HOT_MIN_WAVES) void k_hot_chains(RegionArgs a) {
     __shared__ RegionLds<Codec, true> S;
     hot_chain<Codec, Res, TOK>(a, blockIdx.x, S);
 }
 
-// Phase C (one wave per chunk, all CUs): results of the chunks the chain decided.
+// Phase C (one wave per group of 64 chunks, all CUs): results of the chunks the chains
+// decided. The group's chunk verdicts come in with one load per lane; a chunk holding only
+// the dominant key's records is written without reading them (unless TB balances are out).
 template <class Codec, class Res, bool TOK>
 __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
     __shared__ uint32_t s_base[kHotMax + 1];
     const uint32_t hc = min(a.hot_count[0], kHotMax);
-    const uint32_t total = a.hot_total[0];
-    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].chunk_base;
+    const uint32_t total = a.hot_total[1];
+    for (uint32_t i = threadIdx.x; i < hc; i += 256) s_base[i] = a.hot_info[i].group_base;
     __syncthreads();
     if (a.ctl->span_overflow != 0) return;
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
     const int64_t base = a.ctl->base_ms;
     Res* res = (Res*)a.res;
-    for (uint32_t g = blockIdx.x * 4 + wid; g < total; g += gridDim.x * 4) {
-        const uint32_t i = hot_region_of(s_base, hc, g);
+    for (uint32_t gg = blockIdx.x * 4 + wid; gg < total; gg += gridDim.x * 4) {
+        const uint32_t i = hot_region_of(s_base, hc, gg);
         const HotInfo f = a.hot_info[i];
-        const uint32_t c = g - s_base[i];
-        const uint64_t* s1 = a.hot_summ + (size_t)g * 4;
-        const uint64_t* s2 = a.hot_summ2 + (size_t)(f.group_base + c / 64) * 4;
-        const uint64_t v2 = s2[3], v1 = s1[3];
-        // decided as part of its group (state in the group summary), or on its own
-        const uint64_t* sm = (v2 & 1u) ? s2 : s1;
-        const uint64_t verdict = (v2 & 1u) ? ((v2 & 3u) | (v1 & 0xFF00u)) : v1;
-        if (!(verdict & 1u)) continue;
-        const uint32_t j = f.start + c * kHotChunk + lane;
-        if (j >= f.end) continue;
-        // the hot records here are acquires (n_special == 0); TB permits > max (verdict
-        // bit 1) are the only ones not (deny, 0); other keys' records (bits 8-15) are
-        // k_hot_chain's
+        const uint32_t c0 = (gg - s_base[i]) * 64, c1 = min(c0 + 64, f.n_chunks);
+        const uint64_t* s2 = a.hot_summ2 + (size_t)gg * 8;
+        const uint64_t g0 = s2[3], g1 = s2[7];
+        // lane l: chunk c0 + l's verdict words of both keys
+        const uint64_t* s1l = a.hot_summ + (size_t)(f.chunk_base + min(c0 + lane, c1 - 1)) * 8;
+        const uint64_t cv0 = s1l[3], cv1 = s1l[7];
+        const uint64_t any = __ballot(c0 + lane < c1 && (((g0 | cv0) & 1u) || ((g1 | cv1) & 1u)));
+        if (!any) continue;
         const DevLimiter& L = a.lims[a.region_lim[f.bin]];
-        if (!TOK && !(verdict & 0xFF02u)) {
-            res[j] = (Res)pack_result(false, 0);
-            continue;
+        for (uint64_t m = any; m; m &= m - 1) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+            const uint32_t c = c0 + l;
+            const uint64_t c0w = readlane64(cv0, l), c1w = readlane64(cv1, l);
+            // per key k: decided as part of its group (state in the group summary), or alone
+            const uint64_t v0 = (g0 & 1u) ? ((g0 & 3u) | (c0w & 0xFF00u)) : c0w;
+            const uint64_t v1 = (g1 & 1u) ? (g1 & 3u) : c1w;
+            const uint32_t j = f.start + c * kHotChunk + lane;
+            if (j >= f.end) continue;
+            // the decided keys' records here are acquires (n_special == 0); TB permits > max
+            // (verdict bit 1) are the only ones not (deny, 0); other records are the chains'
+            if (!TOK && (v0 & 1u) && !(v0 & 0xFF02u)) {  // every record is the dominant key's
+                res[j] = (Res)pack_result(false, 0);
+                continue;
+            }
+            const Req q = Codec::dec(recs[j], base);
+            if (q.invalid) continue;
+            const uint64_t* s1 = a.hot_summ + (size_t)(f.chunk_base + c) * 8;
+            const uint64_t* sm;
+            if ((v0 & 1u) && q.h == f.tag) sm = (g0 & 1u) ? s2 : s1;
+            else if ((v1 & 1u) && q.h == f.tag2) sm = ((g1 & 1u) ? s2 : s1) + 4;   // (ok bit 1)
+            else continue;                               // another key
+            const bool early = L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
+            res[j] = (Res)pack_result(false, early ? kRemUnknown : 0);
+            if (TOK) a.tok[j] = (L.algo == kAlgoTB && !early) ? tb_refill(L, q.now_ms, sm[0], sm[1], sm[2])
+                                                             : __builtin_nan("");
         }
-        const Req q = Codec::dec(recs[j], base);
-        if (q.invalid || q.h != f.tag) continue;          // another key (f.ok holds here)
-        const bool early = L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
-        res[j] = (Res)pack_result(false, early ? kRemUnknown : 0);
-        if (TOK) a.tok[j] = (L.algo == kAlgoTB && !early) ? tb_refill(L, q.now_ms, sm[0], sm[1], sm[2])
-                                                         : __builtin_nan("");
     }
 }
 
 template <class Codec, class Res>
 hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs) {
-    if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true>), dim3(kHotMax), dim3(128), 0, hs, a);
-    else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false>), dim3(kHotMax), dim3(128), 0, hs, a);
+    if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true>), dim3(kHotMax), dim3(192), 0, hs, a);
+    else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false>), dim3(kHotMax), dim3(192), 0, hs, a);
     return hipGetLastError();
 }
 template <class Codec, class Res>
 hipError_t regions_combined_t(const RegionArgs& a, hipStream_t s) {
-    const dim3 g(kHotMax + (a.n_regions + 1) / 2), b2(128);
+    const dim3 g(kHotMax + (a.n_regions + 2) / 3), b2(192);
     if (a.tok) hipLaunchKernelGGL((k_regions_hot<Codec, Res, true>), g, b2, 0, s, a);
     else hipLaunchKernelGGL((k_regions_hot<Codec, Res, false>), g, b2, 0, s, a);
     return hipGetLastError();

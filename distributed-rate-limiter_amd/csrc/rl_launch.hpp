@@ -121,8 +121,9 @@ struct RegionArgs {
     const uint32_t* hot_mark;  // [bins] nullable
     uint32_t epoch;
     HotInfo* hot_info;         // [kHotMax]
-    uint64_t* hot_summ;        // [chunks][4]: k_hot_summ's summary, then the chain's verdict
-    uint64_t* hot_summ2;       // [groups][4]: the same over 64 chunks (4096 records)
+    uint64_t* hot_summ;        // [chunks][8]: k_hot_summ's summary, then the chains' verdicts
+                               // (words 0-3 the dominant key, 4-7 the second key)
+    uint64_t* hot_summ2;       // [groups][8]: the same over 64 chunks (4096 records)
     uint32_t* hot_total;       // [0] chunks, [1] groups over the listed regions
     uint32_t* work;            // region walk (walk > 0): 8 claim counters, 64 B apart, zeroed
     uint32_t walk;             // rl_tune("region_walk"): persistent normal-region waves per CU
@@ -182,10 +183,11 @@ struct HotInfo {             // one listed hot region
     uint32_t start, end;     // records [start, end) in bin order
     uint32_t n_chunks;       // ceil((end - start) / kHotChunk)
     uint32_t chunk_base;     // index of its first chunk summary
-    uint32_t ok;             // dominant key seen at least twice in the sample
+    uint32_t ok;             // bit 0: dominant key seen at least twice in the sample;
+                             // bit 1: a second key heavy enough for a chain of its own
     uint32_t n_groups;       // ceil(n_chunks / 64)
     uint32_t group_base;     // index of its first group summary
-    uint32_t pad[2];
+    uint64_t tag2;           // a second dominant key (ok bit 1): its own chain wave
 };
 
 struct BoundsArgs {

@@ -222,3 +222,44 @@ def test_region_order_knob(order):
     tr = trace(35, 800_000, 60_000, 2, 60_000, zipf=1.15, ops=0.01)
     got, want, _ = run(lims, tr, batches=3, capacity=1 << 16, tune={"region_order": order})
     assert_same(got, want, f"region_order={order}")
+
+
+def same_region_keys(n_keys, region_bits, seed):
+    """n_keys distinct key hashes whose tags (mix64) share one region of a table with
+    2^region_bits regions (one shard): the top region_bits bits of mix64(key)."""
+    rng = np.random.default_rng(seed)
+    cand = rng.integers(1, 2**63, 1 << 20, dtype=np.int64).astype(np.uint64)
+    top = rl_amd.mix64(cand) >> np.uint64(64 - region_bits)
+    vals, counts = np.unique(top, return_counts=True)
+    r = vals[np.argmax(counts)]
+    keys = cand[top == r][:n_keys]
+    assert len(keys) == n_keys
+    return keys
+
+
+@pytest.mark.parametrize("algo", ["sw", "tb"])
+@pytest.mark.parametrize("cap_log2", [17, 22])
+def test_hot_two_keys_one_region(algo, cap_log2):
+    # two heavy keys in one region: the dominant one's chain (wave 0), the second's (wave 2)
+    # and every other key of the region (wave 1) at once; one- and two-pass tables (routed)
+    region_bits = max(3, (cap_log2 + 1) - 8)             # capacity * 2 / 256 slots per region
+    lims = [[rl_amd.SW, 500, 30_000, 0.0]] if algo == "sw" else [[rl_amd.TB, 40, 30_000, 6.0]]
+    n = 1_500_000
+    rng = np.random.default_rng(50 + cap_log2)
+    same = same_region_keys(6, region_bits, 51)           # 2 heavy + 4 light keys of that region
+    keys = rl_amd.mix64(rng.integers(0, 100_000, n).astype(np.uint64) + np.uint64(7 << 40))
+    u = rng.random(n)
+    keys[u < 0.30] = same[0]
+    keys[(u >= 0.30) & (u < 0.50)] = same[1]
+    light = (u >= 0.50) & (u < 0.51)
+    keys[light] = same[2 + rng.integers(0, 4, int(light.sum()))]
+    now = (T0 * NS + np.sort(rng.integers(0, 90_000 * NS, n))).astype(np.int64)
+    permits = rng.integers(1, 3, n).astype(np.int32)
+    op = np.zeros(n, np.uint8)
+    v = rng.random(n)
+    op[v < 0.002] = 1
+    op[v < 0.0005] = 2
+    lim = np.zeros(n, np.uint16)
+    tr = (keys, permits, now, lim, op)
+    got, want, _ = run(lims, tr, batches=3, capacity=1 << cap_log2)
+    assert_same(got, want, f"two keys {algo} cap 2^{cap_log2}")
