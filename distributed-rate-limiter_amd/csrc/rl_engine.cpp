@@ -110,6 +110,7 @@ struct rl_engine {
     size_t hot_mark_cap = 0;
     uint32_t epoch = 0;
     uint32_t hot_threshold = 16384;         // rl_tune("hot_threshold"); 0 disables
+    bool hot_thr_auto = true;               // until set: max(hot_threshold, n / 4096) per batch
     // Hot-region routing (two-pass batches): the previous batch's hot regions get pass-0 bins
     // of their own and skip pass 1. route_list holds region ids (kNone = unused); it is built
     // on device at the end of each batch's hot preparation and cleared when region ids change.
@@ -626,6 +627,10 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     // the hot-key path assumes that a denial never changes state; with a local cache a
     // denial may (it puts the estimate, SlidingWindowRateLimiter.java:106-108)
     const bool hot = e->hot_threshold > 0 && bsh == 0 && !cache;
+    // records per region for the hot path: scaled with the batch by default (measured per
+    // config: sw_zipf best at 65536 for 2^28 requests, zipf_1b at 32768 for 2^27)
+    const uint32_t hot_thr = e->hot_thr_auto ? std::max<uint32_t>(e->hot_threshold, (uint32_t)(n >> 12))
+                                             : e->hot_threshold;
     if (hot) {
         rc = ensure_hot_mark(e, n_bins);
         if (rc == RL_OK) rc = ensure_hot_summ(e, n);
@@ -733,7 +738,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         uint32_t* hot_count = e->hot_list + kHotMax;
         HIP_OK(hipMemsetAsync(hot_count, 0, kHotMetaWords * sizeof(uint32_t), s));
         if (route) HIP_OK(launch_hot_route_list(e->route_list, e->route_cnt, e->hot_list, hot_count, s));
-        HIP_OK(launch_hot_select(rstart, rcount, rend, n_bins, e->hot_threshold, e->hot_list,
+        HIP_OK(launch_hot_select(rstart, rcount, rend, n_bins, hot_thr, e->hot_list,
                                  hot_count, e->hot_mark, e->epoch, s));
         ra.hot_list = e->hot_list; ra.hot_count = hot_count; ra.hot_mark = e->hot_mark;
         ra.epoch = e->epoch;
@@ -741,9 +746,6 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 8; ra.hot_total = e->hot_list + kHotMax + kHotTotalOff;
         ra.route_list = e->route_list; ra.route_start = e->route_start; ra.route_cnt = e->route_cnt;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
-        // the next batch's routed regions: this batch's largest hot regions (two-pass tables)
-        if (e->route && passes == 2 && !e->pipeline)
-            HIP_OK(launch_route_next(e->hot_info, hot_count, e->hot_threshold, e->route_list, s));
     }
     if (e->region_order && bsh == 0) {
         if (e->order_cap < n_bins) {
@@ -761,6 +763,9 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
                          e->hot_ev[1]));
     mark(e, 10);
     if (hot) HIP_OK(launch_hot_fill(ra, wide, res_bytes, s));
+    // the next batch's routed regions: this batch's largest hot regions (two-pass tables)
+    if (hot && e->route && passes == 2 && !e->pipeline)
+        HIP_OK(launch_route_next(e->hot_info, e->hot_list + kHotMax, hot_thr, e->route_list, s));
     HIP_OK(launch_stats_reduce(e->d_stats, B.d_ctl, s));
     mark(e, 11);
     mark(e, 8);
@@ -1031,6 +1036,7 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "hot_threshold") == 0) {      // records per region; 0 = no hot path
         if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
         e->hot_threshold = (uint32_t)value;
+        e->hot_thr_auto = false;
         return RL_OK;
     }
     if (std::strcmp(key, "sparse_max") == 0) {         // records per region; 0 = image mode only

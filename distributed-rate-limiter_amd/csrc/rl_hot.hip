@@ -116,47 +116,32 @@ __global__ __launch_bounds__(1024) void k_hot_route_list(const uint32_t* __restr
 }
 
 // The next batch's route table: this batch's listed hot regions with >= threshold records,
-// largest first (ties by list position), each placed at the first free one of its two slots
-// (route_slots) by one thread; at most kRouteMax, a region whose slots are both taken stays
-// unrouted (it is then partitioned normally and found by the hot selection).
+// in list order (largest size class first), each placed at a free one of its two slots
+// (route_slots), 128 entries at a time so that larger regions win the slots; at most
+// kRouteMax. A region whose slots are both taken stays unrouted (it is then partitioned
+// normally and found by the hot selection).
 __global__ __launch_bounds__(1024) void k_route_next(const HotInfo* __restrict__ info,
                                                      const uint32_t* __restrict__ hot_count,
                                                      uint32_t threshold, uint32_t* route_list) {
-    __shared__ uint32_t s_size[kHotMax];
-    __shared__ uint32_t s_rank[kHotMax];             // rank -> list index
     __shared__ uint32_t s_tab[kRouteSlots];
+    __shared__ uint32_t s_placed;
     const uint32_t hc = min(hot_count[0], kHotMax);
     const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < kHotMax; i += blockDim.x) {
-        s_size[i] = i < hc && info[i].end - info[i].start >= threshold ? info[i].end - info[i].start : 0u;
-        s_rank[i] = kNone;
-    }
     for (uint32_t i = t; i < kRouteSlots; i += blockDim.x) s_tab[i] = kNone;
+    if (t == 0) s_placed = 0;
     __syncthreads();
-    for (uint32_t i = t; i < hc; i += blockDim.x) {
-        const uint32_t si = s_size[i];
-        if (si == 0) continue;
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < hc; ++j) {
-            const uint32_t sj = s_size[j];
-            rank += (sj > si || (sj == si && j < i)) ? 1u : 0u;
-        }
-        s_rank[rank] = i;
-    }
-    __syncthreads();
-    if (t == 0) {
-        uint32_t placed = 0;
-        for (uint32_t r = 0; r < hc && placed < kRouteMax; ++r) {
-            const uint32_t i = s_rank[r];
-            if (i == kNone) break;                   // ranks of eligible entries are dense
+    for (uint32_t b0 = 0; b0 < hc; b0 += 128) {
+        const uint32_t i = b0 + t;
+        if (t < 128 && i < hc && info[i].end - info[i].start >= threshold) {
             const uint32_t b = info[i].bin;
             uint32_t s1, s2;
             route_slots(b, s1, s2);
-            if (s_tab[s1] == kNone) { s_tab[s1] = b; ++placed; }
-            else if (s_tab[s2] == kNone) { s_tab[s2] = b; ++placed; }
+            if (atomicCAS(&s_tab[s1], kNone, b) == kNone || atomicCAS(&s_tab[s2], kNone, b) == kNone)
+                atomicAdd(&s_placed, 1u);
         }
+        __syncthreads();
+        if (s_placed >= kRouteMax) break;              // (block-uniform)
     }
-    __syncthreads();
     for (uint32_t i = t; i < kRouteSlots; i += blockDim.x) route_list[i] = s_tab[i];
 }
 

@@ -210,6 +210,8 @@ struct UnpermArgs {
     const uint32_t* pos0;
     const uint32_t* pos1;      // nullable
     const void* res;
+    const void* res_hi;        // (set by launch_unpermute) two-pass: results at positions >=
+                               // ctl->n_normal (routed records), read in place
     const double* tok;         // nullable
     void* mid;                 // nullable: n results of scratch (two-pass batches)
     const int64_t* ext;        // escaped remainders, indexed like res (before `mid`)

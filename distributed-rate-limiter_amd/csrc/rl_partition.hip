@@ -144,14 +144,17 @@ template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     using Rec = typename Codec::Rec;
     static_assert(kTileThreads / 64 <= 8, "per-wave counts are packed 8 to a bin");
-    __shared__ uint32_t cur[1u << kMaxDigitBits];                    // next slot per bin
+    // dynamic LDS (scatter_lds_bytes): per bin, this round's per-wave counts packed in one
+    // word (cntw), then the next slot (cur); sized to the pass's bins
+    extern __shared__ uint64_t dyn_lds64[];
     // this round's count of each wave per bin, the waves' bytes packed in one word: a lane
     // sums the earlier waves' counts for its bin with one read and two v_sad_u8
-    __shared__ uint64_t cntw[1u << kMaxDigitBits];
     __shared__ LimLds L;
     __shared__ uint64_t s_mm[2][kTileThreads / 64];
     const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
+    uint64_t* cntw = dyn_lds64;
+    uint32_t* cur = (uint32_t*)(dyn_lds64 + bins);
     load_lim_lds(L, a);
     int64_t base = 0;
     if constexpr (RAW) base = a.ctl->base_ms;
@@ -347,6 +350,10 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
   constexpr int B = 8;                         // rounds per batch (loads issued together)
   constexpr int NB = kTileItems / B;
   const bool simple = pos1 || a.tokens_out || (a.ablate & kAblNoGather);
+  // two-pass batches: mid (res) holds the normal records' results in pass-0 order, res_hi
+  // the routed records' results at their own (pass-0) positions >= n_normal
+  const Res* __restrict__ res_hi = (const Res*)a.res_hi;
+  const uint32_t nn = res_hi ? a.ctl->n_normal : 0u;
   for (uint32_t it = 0;; ++it) {
     const uint32_t tile = tile_at(it, a.n_tiles);
     if (tile >= a.n_tiles) break;
@@ -363,7 +370,7 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
         };
         auto gather = [&](Res (&v)[B], const uint32_t (&p)[B]) {
 #pragma unroll
-            for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+            for (int k = 0; k < B; ++k) v[k] = (res_hi && p[k] >= nn ? res_hi : res)[p[k]];
         };
         auto store = [&](const Res (&v)[B], int b) {
 #pragma unroll
@@ -404,7 +411,7 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
             for (int k = 0; k < B; ++k) v[k] = (Res)p[k];
         } else {
 #pragma unroll
-            for (int k = 0; k < B; ++k) v[k] = res[p[k]];
+            for (int k = 0; k < B; ++k) v[k] = (res_hi && p[k] >= nn ? res_hi : res)[p[k]];
         }
 #pragma unroll
         for (int k = 0; k < B; ++k) {
@@ -446,7 +453,8 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
 // whole result array. k_unpermute then gathers mid[pos0[i]] (2^d0 streams). Two
 // local gathers replace the composed res[pos1[pos0[i]]], which hit a random line of a
 // 1 GB index and of the result array per request.
-// Routed records (pass-0 positions >= ctl->n_normal) skipped pass 1: mid[j] = res[j].
+// Routed records (pass-0 positions >= ctl->n_normal) skipped pass 1: k_unpermute reads
+// their results in place (UnpermArgs::res_hi), so mid covers the normal records only.
 template <class Res>
 __global__ __launch_bounds__(256) void k_unpermute_mid(const uint32_t* __restrict__ pos1,
                                                        const Res* __restrict__ res,
@@ -454,12 +462,13 @@ __global__ __launch_bounds__(256) void k_unpermute_mid(const uint32_t* __restric
                                                        const BatchCtl* __restrict__ ctl) {
     constexpr int B = 8;
     const uint32_t base = blockIdx.x * (256u * B) + threadIdx.x;
-    const uint32_t nn = ctl->n_normal;
+    n = min(n, ctl->n_normal);
+    if (base >= n) return;
     uint32_t p[B];
 #pragma unroll
     for (int k = 0; k < B; ++k) {
         const uint32_t j = base + (uint32_t)k * 256u;
-        p[k] = j < nn ? pos1[j] : j < n ? j : 0;
+        p[k] = pos1[j < n ? j : base];
     }
     Res v[B];
 #pragma unroll
@@ -498,12 +507,15 @@ hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s)
 
 hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s) {
     dim3 grid(persistent_grid(a.n_tiles, a.sc_per_cu ? a.sc_per_cu : 1)), block(kTileThreads);
+    const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
+    if (bins > (1u << kMaxDigitBits)) return hipErrorInvalidValue;
+    const size_t lds = bins * (sizeof(uint64_t) + sizeof(uint32_t));
     if (raw) {
-        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, 0, s, a);
+        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, lds, s, a);
     } else {
-        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, false>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_scatter<CodecC, false>), grid, block, 0, s, a);
+        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_scatter<CodecC, false>), grid, block, lds, s, a);
     }
     return hipGetLastError();
 }
@@ -588,6 +600,7 @@ hipError_t launch_unpermute(const UnpermArgs& a_in, int res_bytes, hipStream_t s
         else if (res_bytes == 1) unpermute_mid<uint8_t>(a, s);
         else if (res_bytes == 2) unpermute_mid<uint16_t>(a, s);
         else unpermute_mid<uint32_t>(a, s);
+        a.res_hi = a.res;
         a.res = a.mid;
         a.pos1 = nullptr;
     }

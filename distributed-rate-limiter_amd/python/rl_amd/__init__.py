@@ -235,6 +235,11 @@ class Engine:
             raise RlError(st, "rl_create")
         self._h = h
         self.limiters = []
+        # RL_TUNE="key=value,...": engine knobs for every engine of the process (A/B and
+        # diagnostics runs of the test suite; every setting gives the same decisions)
+        for kv in filter(None, os.environ.get("RL_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            self.tune(k.strip(), int(v))
 
     def close(self):
         if getattr(self, "_h", None):

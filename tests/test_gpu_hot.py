@@ -263,3 +263,28 @@ def test_hot_two_keys_one_region(algo, cap_log2):
     tr = (keys, permits, now, lim, op)
     got, want, _ = run(lims, tr, batches=3, capacity=1 << cap_log2)
     assert_same(got, want, f"two keys {algo} cap 2^{cap_log2}")
+
+
+def test_hot_routed_device_entry_ragged():
+    # device entry without balances (the unpermute's two-level gather: normal records through
+    # pass 1, routed ones read in place), ragged batch sizes (partial last tiles)
+    import torch
+    lims = [[rl_amd.SW, 300, 30_000, 0.0], [rl_amd.TB, 30, 20_000, 5.0]]
+    tr = hot_trace(36, 1_700_000, 300_000, 0.5, [0, 1], 90_000, hot_keys=6)
+    e = rl_amd.Engine(max_batch=1 << 20, capacity=1 << 22)
+    for l in lims:
+        e.add_limiter(*l)
+    cuts = [0, 333_333, 833_334, 1_611_111, 1_700_000]
+    ga, gr = [], []
+    for b in range(len(cuts) - 1):
+        sl = slice(cuts[b], cuts[b + 1])
+        m = cuts[b + 1] - cuts[b]
+        k, p, t, li = (torch.from_numpy(np.ascontiguousarray(x[sl])).cuda()
+                       for x in (tr[0].view(np.int64), tr[1], tr[2], tr[3].view(np.int16)))
+        a = torch.empty(m, dtype=torch.uint8, device="cuda")
+        r = torch.empty(m, dtype=torch.int64, device="cuda")
+        e.execute_device(m, k, p, t, li, None, a, r)
+        assert e.last_status() in (rl_amd.RL_OK, rl_amd.RL_E_INVALID_REQUEST)
+        ga.append(a.cpu().numpy()); gr.append(r.cpu().numpy())
+    want = COracle(lims).run(*tr[:4])
+    assert_same((np.concatenate(ga), np.concatenate(gr), None), want, "routed device ragged")

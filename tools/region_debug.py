@@ -73,6 +73,10 @@ for b in range(args.batches):
                 if hot[i] else f"rounds {rr:8d}")
         print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  lim {lim_of[i]} "
               f"recs {int(d[i, 2]):9d} {what}")
+    late = np.argsort(-(d[:, 1].astype(np.int64)))[:6]
+    print("   latest ends: " + "; ".join(
+        f"{'hot' if hot[i] else 'normal'} recs {int(d[i, 2])} start {(d[i, 0] - t0) / 100:.0f} "
+        f"end {(d[i, 1] - t0) / 100:.0f} us" for i in late))
     nh = ~hot
     ends = (d[nh, 1] - t0) / 100
     for q in ((0.5, 0.9, 0.99, 0.999, 1.0) if nh.any() else ()):
