@@ -282,6 +282,94 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         same_w = ((wi & 1) ? b0 : ~b0) & ((wi & 2) ? b1 : ~b1);
         elig_m = __ballot(slot >= 0 && wi < 3 && q.op == (uint32_t)kOpAcquire);
     }
+    if constexpr (!tb && !CACHE) {
+        // Sliding window: a greedy scan per key instead of one round per state change. Inside
+        // the window W0 of a key's first pending request, its acquires only INCR the current
+        // bucket (:114-116), so with k allows before it a request's estimate is
+        // d2l(tv + (C0 + k)), tv = prev * pw at its own time (:174): it is allowed iff k <= K,
+        // its largest such k (denials change nothing, :104-111). One pass computes K per lane;
+        // the allows then follow by integer compares (the j-th allow of a key is its first
+        // request after the (j-1)-th with K >= j - 1), every key of the group at once. The
+        // first request of a key the scan cannot take (another window, before the key's newest
+        // bucket, near the epoch, a peek or a reset) runs the exact step alone; its later
+        // requests go to the next pass. (The rounds below remain for the token bucket, whose
+        // allows are a sequential fp64 recurrence, and for the local cache.)
+        {
+            const int64_t w = L.window_ms, mx = L.max_permits;
+            while (__any(pending)) {
+                ++n_rounds;
+                const uint64_t kp = peers & __ballot(pending);
+                const uint32_t f0 = kp ? (uint32_t)__builtin_ctzll(kp) : lane;
+                const int64_t W0 = __shfl(geo.curr_start, (int)f0, 64);
+                uint64_t sa = 0, sb = 0, sc = 0;
+                if (pending) { sa = S.sa[slot]; sb = S.sb[slot]; sc = S.sc[slot]; }
+                const bool scan = pending && q.op == (uint32_t)kOpAcquire && geo.curr_start == W0 &&
+                                  (int64_t)sa <= W0 && geo.prev_start != geo.curr_start;
+                const uint64_t und = __ballot(pending && !scan) & peers;
+                const uint32_t stop = und ? (uint32_t)__builtin_ctzll(und) : 64u;
+                const bool in = scan && lane < stop;
+                const SW2 s0 = sw_unpack(sa, sb, sc);
+                const int64_t C0 = s0.b1_start == W0 ? (int64_t)s0.b1_cnt : 0;
+                double tv = 0.0;
+                int64_t K = -1;
+                auto est = [&](int64_t kk) { return d2l(tv + (double)(C0 + kk)); };
+                if (in) {
+                    const int64_t P = sw_get(s0, geo.prev_start, q.now_ms, w);
+                    tv = (double)P * geo.prev_weight;                      // :174, rounded
+                    K = mx - (int64_t)q.permits - C0 - (int64_t)tv;        // ~ largest k
+                    if (K >= 0 && est(K) + q.permits > mx) --K;           // rounding edges
+                    if (K >= 0 && est(K) + q.permits > mx) --K;
+                    if (est(K + 1) + q.permits <= mx) ++K;
+                    if (K < -1) K = -1;
+                }
+                // greedy scan: kk = the key's allows before this request
+                uint32_t cur = 0, last = 64u;
+                int64_t k = 0, kk = 0;
+                bool al = false, done = !in;
+                for (;;) {
+                    const bool c = in && !done && lane >= cur;
+                    const uint64_t mk = __ballot(c && K >= k) & peers;
+                    if (c) kk = k;
+                    if (!done && mk == 0) done = true;
+                    if (!__any(!done)) break;
+                    if (!done) {
+                        const uint32_t fa = (uint32_t)__builtin_ctzll(mk);
+                        if (lane == fa) al = true;
+                        last = fa;
+                        ++k;
+                        cur = fa + 1;
+                    }
+                }
+                if (in) {
+                    const int64_t e = est(al ? kk + 1 : kk);                // after the request
+                    r.alw = al;
+                    r.rem = mx - e > 0 ? mx - e : 0;
+                    r.tok = __builtin_nan("");
+                    n_allowed += al ? 1u : 0u;
+                    pending = false;
+                }
+                if (al && lane == last) {                 // the key's last allow commits them all
+                    SWGeo gl{};
+                    gl.curr_start = W0;
+                    sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)k, q.now_ms);
+                    S.sa[slot] = sa; S.sb[slot] = sb; S.sc[slot] = sc;
+                }
+                wave_fence();
+                if (pending && lane == stop) {            // the exact step, after the scan's allows
+                    const Outcome o = sw_step_g(L, q.op, q.permits, q.now_ms, geo, S.sa[slot],
+                                                S.sb[slot], S.sc[slot]);
+                    if (o.mutate) { S.sa[slot] = o.a; S.sb[slot] = o.b; S.sc[slot] = o.c; }
+                    r.alw = o.allowed;
+                    r.rem = o.remaining;
+                    r.tok = __builtin_nan("");
+                    n_allowed += o.allowed ? 1u : 0u;
+                    pending = false;
+                }
+                wave_fence();
+            }
+        }
+        return r;
+    } else {
     [[maybe_unused]] uint32_t my_rounds = 0;      // -DRL_CHAINS only
     while (__any(pending)) {
         // Chains: after two rounds, if every key still pending has changed state in (nearly)
@@ -405,6 +493,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         wave_fence();
     }
     return r;
+    }
 }
 
 template <class Codec, class Res, bool TOK, int BS, class LdsT>

@@ -103,7 +103,7 @@ def build(force: bool = False) -> str:
     """Compile librl_engine.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
     if force:
         subprocess.check_call(["make", "-s", "-C", PKG_DIR, "clean"])
-    subprocess.check_call(["make", "-s", "-j4", "-C", PKG_DIR])    # make skips up-to-date targets
+    subprocess.check_call(["make", "-s", "-j8", "-C", PKG_DIR])    # make skips up-to-date targets
     return LIB_PATH
 
 
