@@ -96,8 +96,9 @@ struct rl_engine {
     bool pipeline = false;                  // RL_OPT_PIPELINE
     hipStream_t pstream = nullptr;          // partition stream (pipeline)
     hipEvent_t in_ev = nullptr;             // pipeline: inputs ready on e->stream
-    hipStream_t hstream = nullptr;          // hot chains beside the normal regions
-    hipEvent_t hot_ev[2] = {};              // fork / join of hstream
+    hipStream_t hstream = nullptr;          // hot chains beside the normal regions (one key)
+    hipStream_t hstream2 = nullptr;         // ... (two keys: 3-wave workgroups)
+    hipEvent_t hot_ev[3] = {};              // fork, joins of hstream / hstream2
     bool split_hot = true;                  // rl_tune("split_hot"): 0 = one 2-wave launch
     uint32_t region_walk = 0;               // rl_tune("region_walk"): persistent waves per CU
     uint32_t* d_work = nullptr;             // its claim counters (8 x 64 B)
@@ -259,8 +260,10 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
     if (hipStreamCreateWithPriority(&e->hstream, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&e->hstream2, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
         hipEventCreateWithFlags(&e->hot_ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->hot_ev[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&e->hot_ev[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->hot_ev[2], hipEventDisableTiming) != hipSuccess) {
         rl_destroy(e);
         return RL_E_DEVICE;
     }
@@ -310,6 +313,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->pstream) (void)hipStreamSynchronize(e->pstream);
     if (e->hstream) (void)hipStreamSynchronize(e->hstream);
+    if (e->hstream2) (void)hipStreamSynchronize(e->hstream2);
     for (auto& l : e->lims) { dfree(l.table); dfree(l.cache_table); }
     dfree(e->d_lims); dfree(e->d_region_lim);
     for (BatchScratch& B : e->sc) {
@@ -336,6 +340,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     if (e->pstream) (void)hipStreamDestroy(e->pstream);
     if (e->in_ev) (void)hipEventDestroy(e->in_ev);
     if (e->hstream) (void)hipStreamDestroy(e->hstream);
+    if (e->hstream2) (void)hipStreamDestroy(e->hstream2);
     for (hipEvent_t ev : e->hot_ev) if (ev) (void)hipEventDestroy(ev);
     delete e;
 }
@@ -760,7 +765,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     mark(e, 7);
     // hot chains first (side stream), then the regions
     HIP_OK(launch_region(ra, wide, res_bytes, s, e->split_hot ? e->hstream : nullptr, e->hot_ev[0],
-                         e->hot_ev[1]));
+                         e->hot_ev[1], e->split_hot ? e->hstream2 : nullptr, e->hot_ev[2]));
     mark(e, 10);
     if (hot) HIP_OK(launch_hot_fill(ra, wide, res_bytes, s));
     // the next batch's routed regions: this batch's largest hot regions (two-pass tables)

@@ -326,8 +326,11 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
 // wave_apply. The passes touch disjoint slots of the shared LDS table (wave 0 only the
 // hot key's state, wave 1 never that slot), so they need no synchronisation. Wave 2 runs
 // pass 1 for a second dominant key when the region holds one (HotInfo::ok bit 1); wave 1
-// then applies the records of neither key.
-template <class Codec, class Res, bool TOK>
+// then applies the records of neither key. WAVES = 1 (split launch, regions without a second
+// key): one wave runs pass 1 and then pass 2. A single-wave workgroup takes the first wave
+// slot that frees beside the normal regions; a 3-wave one waited for three on one CU, and
+// the later chains of sw_zipf started ~4 ms into the stage.
+template <class Codec, class Res, bool TOK, int WAVES = 3>
 __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Codec, true>& S) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
@@ -338,6 +341,11 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     // the passes are sequential critical paths beside thousands of normal-region waves
     __builtin_amdgcn_s_setprio(3);
     const HotInfo f = a.hot_info[i];
+    if constexpr (WAVES == 1) {
+        if (f.ok & 2u) return;                        // two keys: the 3-wave launch's
+    } else {
+        if (a.chain_split && !(f.ok & 2u)) return;    // one key: the 1-wave launch's
+    }
     const uint32_t region = f.bin;                    // bin_shift 0: bin == region
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
@@ -789,7 +797,15 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         if (count > 0) apply64(count);
         if (a.dbg) cyc_pass2 += __builtin_amdgcn_s_memtime() - c_p2;
     };
-    if (wid == 0 || wid == 2) {
+    if constexpr (WAVES == 1) {
+        if (L.algo == kAlgoTB) {
+            if (hot_ok) pass1(std::integral_constant<int, kAlgoTB>{}, 0u);
+            pass2(std::integral_constant<int, kAlgoTB>{});
+        } else {
+            if (hot_ok) pass1(std::integral_constant<int, kAlgoSW>{}, 0u);
+            pass2(std::integral_constant<int, kAlgoSW>{});
+        }
+    } else if (wid == 0 || wid == 2) {
         const uint32_t kk = wid >> 1;
         if (kk ? hot_ok2 : hot_ok) {
             if (L.algo == kAlgoTB) pass1(std::integral_constant<int, kAlgoTB>{}, kk);
@@ -812,7 +828,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     }
     // ---- write the region back, statistics
     __shared__ uint64_t s_w1[2];                      // wave 1's debug counters
-    if (wid == 1 && lane == 0) { s_w1[0] = n_other; s_w1[1] = cyc_pass2; }
+    if (wid == (WAVES == 1 ? 0u : 1u) && lane == 0) { s_w1[0] = n_other; s_w1[1] = cyc_pass2; }
     const bool touched0 = __syncthreads_or(wid == 0 && any_hot);
     const bool touched1 = __syncthreads_or(wid == 2 && any_hot);
     if (wid != 0) return;
@@ -866,10 +882,10 @@ __global__ __launch_bounds__(192, RL_HOT_MIN_WAVES) void k_regions_hot(RegionArg
 // The hot chains alone (3-wave workgroups), launched on a side stream just before the
 // normal regions' single-wave launch: no normal region waits for another region of a
 // multi-wave workgroup, and the chains still start first.
-template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(192, RL_HOT_MIN_WAVES) void k_hot_chains(RegionArgs a) {
+template <class Codec, class Res, bool TOK, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, RL_HOT_MIN_WAVES) void k_hot_chains(RegionArgs a) {
     __shared__ RegionLds<Codec, true> S;
-    hot_chain<Codec, Res, TOK>(a, blockIdx.x, S);
+    hot_chain<Codec, Res, TOK, WAVES>(a, blockIdx.x, S);
 }
 
 // Phase C (one wave per group of 64 chunks, all CUs): results of the chunks the chains
@@ -929,10 +945,19 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
     }
 }
 
+// Split launch: single-key regions' chains as 1-wave workgroups on hs, two-key regions' as
+// 3-wave workgroups on hs2 (each launch skips the other's entries).
 template <class Codec, class Res>
-hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs) {
-    if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true>), dim3(kHotMax), dim3(192), 0, hs, a);
-    else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false>), dim3(kHotMax), dim3(192), 0, hs, a);
+hipError_t hot_chains_t(const RegionArgs& a_in, hipStream_t hs, hipStream_t hs2) {
+    RegionArgs a = a_in;
+    a.chain_split = 1;
+    if (a.tok) {
+        hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 1>), dim3(kHotMax), dim3(64), 0, hs, a);
+        hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
+    } else {
+        hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 1>), dim3(kHotMax), dim3(64), 0, hs, a);
+        hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
+    }
     return hipGetLastError();
 }
 template <class Codec, class Res>

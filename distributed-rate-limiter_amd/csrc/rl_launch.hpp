@@ -134,6 +134,7 @@ struct RegionArgs {
     // region order[g]; order[n_regions] = number of non-empty regions listed)
     const uint32_t* order;
     uint32_t order_prefix;     // that many of the smallest regions are dispatched first
+    uint32_t chain_split;      // (set by the launcher) hot chains in two launches by key count
     // routed hot regions (hot_list entries with kHotRoutedBit): region, first record, count
     const uint32_t* route_list;
     const uint32_t* route_start;
@@ -286,14 +287,16 @@ hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t ro
 // hs (nullable): side stream for the hot chains (k_hot_chains), ordered by events e0 / e1;
 // without it the chains share the normal regions' launch (2-wave workgroups).
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
-                         hipStream_t hs = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                         hipStream_t hs = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
+                         hipStream_t hs2 = nullptr, hipEvent_t e2 = nullptr);
 // the hot chains' side-stream launch, and the one-launch variant (split_hot 0)
-hipError_t launch_hot_chains(const RegionArgs& a, bool wide, int res_bytes, hipStream_t hs);
+hipError_t launch_hot_chains(const RegionArgs& a, bool wide, int res_bytes, hipStream_t hs, hipStream_t hs2);
 hipError_t launch_regions_combined(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
 // per record codec / packed result width (instantiated in csrc/rl_rt_*.hip)
 template <class Codec, class Res>
-hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0, hipEvent_t e1);
-template <class Codec, class Res> hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs);
+hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0, hipEvent_t e1,
+                           hipStream_t hs2, hipEvent_t e2);
+template <class Codec, class Res> hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs, hipStream_t hs2);
 template <class Codec, class Res> hipError_t regions_combined_t(const RegionArgs& a, hipStream_t s);
 template <class Codec, class Res> hipError_t hot_fill_t(const RegionArgs& a, hipStream_t s);
 hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s);

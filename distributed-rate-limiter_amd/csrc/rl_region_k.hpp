@@ -47,12 +47,13 @@ __global__ __launch_bounds__(64, RL_REGION_MIN_WAVES) void k_regions_walk(Region
 
 template <class Codec, class Res>
 hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0,
-                           hipEvent_t e1) {
+                           hipEvent_t e1, hipStream_t hs2, hipEvent_t e2) {
     const dim3 b(64);
-    if (a.bin_shift == 0 && a.hot_mark && hs) {          // hot chains beside normal regions
+    if (a.bin_shift == 0 && a.hot_mark && hs && hs2) {          // hot chains beside normal regions
         (void)hipEventRecord(e0, s);
         (void)hipStreamWaitEvent(hs, e0, 0);
-        (void)hot_chains_t<Codec, Res>(a, hs);
+        (void)hipStreamWaitEvent(hs2, e0, 0);
+        (void)hot_chains_t<Codec, Res>(a, hs, hs2);
         if (a.walk && a.work) {
             const uint32_t grid = persistent_grid(a.n_regions, a.walk);
             const uint32_t chunk = std::max<uint32_t>(1u, a.n_regions / (grid * 32u));
@@ -65,7 +66,9 @@ hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, h
             else hipLaunchKernelGGL((k_regions<Codec, Res, false, 0>), g, b, 0, s, a);
         }
         (void)hipEventRecord(e1, hs);
+        (void)hipEventRecord(e2, hs2);
         (void)hipStreamWaitEvent(s, e1, 0);
+        (void)hipStreamWaitEvent(s, e2, 0);
     } else if (a.bin_shift == 0 && a.hot_mark) {         // hot chains + normal regions
         (void)regions_combined_t<Codec, Res>(a, s);
     } else if (a.bin_shift == 0 && a.cache) {

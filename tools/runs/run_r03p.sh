@@ -1,0 +1,12 @@
+#!/bin/bash
+# double-buffered upsweep loads; partition tests; bench sw_zipf + zipf_1b; sw_zipf region timeline
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hot.py tests/test_gpu_configs.py tests/test_gpu_sparse.py -x -q --timeout 300 --timeout-method thread > gpurun_out/t_p.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" gpurun_out/t_p.log | head -20; tail -20 gpurun_out/t_p.log; exit 1; }
+tail -1 gpurun_out/t_p.log
+for cfg in sw_zipf zipf_1b tb_uniform; do
+  timeout -k 10 300 python -u bench.py --config $cfg --no-cpu-baseline --no-extra --steps 6 > gpurun_out/b_p_${cfg}.log 2>&1 || { echo "bench $cfg failed"; tail -5 gpurun_out/b_p_${cfg}.log; exit 1; }
+  tail -1 gpurun_out/b_p_${cfg}.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$cfg', '%.3e'%d['value'], 'ms/step %.2f'%d['ms_per_step'], {k: round(v,2) for k,v in d['stage_ms'].items()})"
+done
+timeout -k 10 200 python -u tools/region_debug.py --config sw_zipf --batches 3 > gpurun_out/rd_p.log 2>&1 || { echo "region_debug failed"; tail -5 gpurun_out/rd_p.log; exit 1; }
+grep -E "batch|quantile|latest|normal: sum" gpurun_out/rd_p.log
