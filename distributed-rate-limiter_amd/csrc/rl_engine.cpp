@@ -118,6 +118,8 @@ struct rl_engine {
     bool route = true;                      // rl_tune("route")
     bool region_order = true;               // rl_tune("region_order"): largest regions dispatched first
     uint32_t order_prefix = 4096;           // rl_tune("order_prefix"): ... after this many of the smallest
+    bool chain3 = false;                    // rl_tune("chain3"): two-key hot regions as 3-wave workgroups
+                                            // (0: single waves run both keys' passes; measured faster)
     uint32_t* order = nullptr;              // [order_cap + 1]
     size_t order_cap = 0;
     uint32_t* order_meta = nullptr;         // [kOrderMeta]
@@ -730,6 +732,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.walk = e->region_walk;
     ra.cache = cache ? 1u : 0u;
     ra.sparse_max = bsh == 0 ? e->sparse_max : 0u;
+    ra.chain3 = e->chain3 ? 1u : 0u;
     if (e->debug_regions) {
         if (e->dbg_cap < (size_t)n_bins * kDbgWords) {
             dfree(e->dbg);
@@ -1056,6 +1059,10 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "region_order") == 0) {
         e->region_order = value != 0;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "chain3") == 0) {
+        e->chain3 = value != 0;
         return RL_OK;
     }
     if (std::strcmp(key, "order_prefix") == 0) {

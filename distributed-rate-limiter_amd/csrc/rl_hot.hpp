@@ -342,9 +342,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     __builtin_amdgcn_s_setprio(3);
     const HotInfo f = a.hot_info[i];
     if constexpr (WAVES == 1) {
-        if (f.ok & 2u) return;                        // two keys: the 3-wave launch's
+        if (a.chain_split == 2 && (f.ok & 2u)) return;   // two keys: the 3-wave launch's
     } else {
-        if (a.chain_split && !(f.ok & 2u)) return;    // one key: the 1-wave launch's
+        if (a.chain_split && !(f.ok & 2u)) return;       // one key: the 1-wave launch's
     }
     const uint32_t region = f.bin;                    // bin_shift 0: bin == region
     const DevLimiter L = a.lims[a.region_lim[region]];
@@ -800,9 +800,11 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     if constexpr (WAVES == 1) {
         if (L.algo == kAlgoTB) {
             if (hot_ok) pass1(std::integral_constant<int, kAlgoTB>{}, 0u);
+            if (hot_ok2) pass1(std::integral_constant<int, kAlgoTB>{}, 1u);
             pass2(std::integral_constant<int, kAlgoTB>{});
         } else {
             if (hot_ok) pass1(std::integral_constant<int, kAlgoSW>{}, 0u);
+            if (hot_ok2) pass1(std::integral_constant<int, kAlgoSW>{}, 1u);
             pass2(std::integral_constant<int, kAlgoSW>{});
         }
     } else if (wid == 0 || wid == 2) {
@@ -830,7 +832,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     __shared__ uint64_t s_w1[2];                      // wave 1's debug counters
     if (wid == (WAVES == 1 ? 0u : 1u) && lane == 0) { s_w1[0] = n_other; s_w1[1] = cyc_pass2; }
     const bool touched0 = __syncthreads_or(wid == 0 && any_hot);
-    const bool touched1 = __syncthreads_or(wid == 2 && any_hot);
+    const bool touched1 = __syncthreads_or((WAVES == 1 ? wid == 0 : wid == 2) && any_hot);
     if (wid != 0) return;
     if (lane == 0 && hot_ok && touched0) S.occ[hsl0] |= 2u;
     if (lane == 0 && hot_ok2 && touched1) S.occ[hsl1] |= 2u;
@@ -950,13 +952,13 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
 template <class Codec, class Res>
 hipError_t hot_chains_t(const RegionArgs& a_in, hipStream_t hs, hipStream_t hs2) {
     RegionArgs a = a_in;
-    a.chain_split = 1;
+    a.chain_split = a_in.chain3 ? 2u : 1u;      // chain3 0: single waves take every region
     if (a.tok) {
         hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 1>), dim3(kHotMax), dim3(64), 0, hs, a);
-        hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
+        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
     } else {
         hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 1>), dim3(kHotMax), dim3(64), 0, hs, a);
-        hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
+        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
     }
     return hipGetLastError();
 }

@@ -134,7 +134,9 @@ struct RegionArgs {
     // region order[g]; order[n_regions] = number of non-empty regions listed)
     const uint32_t* order;
     uint32_t order_prefix;     // that many of the smallest regions are dispatched first
-    uint32_t chain_split;      // (set by the launcher) hot chains in two launches by key count
+    uint32_t chain_split;      // (set by the launcher) 1: single-wave chains take every region;
+                               // 2: two-key regions go to the 3-wave launch
+    uint32_t chain3;           // rl_tune("chain3"): two-key regions as 3-wave workgroups
     // routed hot regions (hot_list entries with kHotRoutedBit): region, first record, count
     const uint32_t* route_list;
     const uint32_t* route_start;
