@@ -159,6 +159,7 @@ struct rl_engine {
     bool timing = false;
     bool last_wide = false;
     bool pending_status = false;
+    uint32_t hot_hint = 0xFFFFFFFFu;        // hot regions of the last batch seen complete
     int last_status = RL_OK;
     uint64_t last_n = 0;
     uint32_t ablate = 0;                    // rl_tune("ablate"), measurement only
@@ -733,6 +734,13 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.cache = cache ? 1u : 0u;
     ra.sparse_max = bsh == 0 ? e->sparse_max : 0u;
     ra.chain3 = e->chain3 ? 1u : 0u;
+    // chain launch size: twice the hot count of the last batch the host saw complete (a
+    // hint only: the chains loop over the hot list with the grid's stride), the whole
+    // kHotMax before any batch has completed
+    if (e->hot_hint != 0xFFFFFFFFu) {
+        const uint32_t nh = e->hot_hint;
+        ra.chain_grid = nh ? std::min<uint32_t>(kHotMax, std::max<uint32_t>(256u, 2u * nh)) : 64u;
+    }
     if (e->debug_regions) {
         if (e->dbg_cap < (size_t)n_bins * kDbgWords) {
             dfree(e->dbg);
@@ -806,6 +814,7 @@ static int collect_status(rl_engine* e) {
     if (!e->pending_status) return e->last_status;
     e->pending_status = false;
     const BatchCtl& c = *e->h_ctl;
+    e->hot_hint = c.n_hot;
     int st = RL_OK;
     if (c.invalid) st = RL_E_INVALID_REQUEST;
     if (c.cap_err) st = RL_E_CAPACITY;
@@ -1088,8 +1097,10 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
 
 extern "C" int rl_sync(rl_engine* e) {
     if (!e) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
     HIP_OK(hipStreamSynchronize(e->stream));
     if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
+    if (e->pending_status) e->hot_hint = e->h_ctl->n_hot;    // the last batch is complete
     return RL_OK;
 }
 

@@ -162,6 +162,7 @@ template <class Codec>
 __global__ __launch_bounds__(64) void k_hot_prep(RegionArgs a) {
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     const uint32_t i = blockIdx.x, lane = threadIdx.x;
+    if (i == 0 && lane == 0) a.ctl->n_hot = hc;
     if (i >= hc) return;
     const uint32_t e = a.hot_list[i];
     uint32_t bin, start, end;
@@ -887,7 +888,11 @@ __global__ __launch_bounds__(192, RL_HOT_MIN_WAVES) void k_regions_hot(RegionArg
 template <class Codec, class Res, bool TOK, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, RL_HOT_MIN_WAVES) void k_hot_chains(RegionArgs a) {
     __shared__ RegionLds<Codec, true> S;
-    hot_chain<Codec, Res, TOK, WAVES>(a, blockIdx.x, S);
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    for (uint32_t i = blockIdx.x; i < hc; i += gridDim.x) {       // (workgroup-uniform)
+        if (i != blockIdx.x) __syncthreads();                     // the last chain's LDS users
+        hot_chain<Codec, Res, TOK, WAVES>(a, i, S);
+    }
 }
 
 // Phase C (one wave per group of 64 chunks, all CUs): results of the chunks the chains
@@ -953,12 +958,13 @@ template <class Codec, class Res>
 hipError_t hot_chains_t(const RegionArgs& a_in, hipStream_t hs, hipStream_t hs2) {
     RegionArgs a = a_in;
     a.chain_split = a_in.chain3 ? 2u : 1u;      // chain3 0: single waves take every region
+    const dim3 g(a.chain_grid ? min(a.chain_grid, kHotMax) : kHotMax);
     if (a.tok) {
-        hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 1>), dim3(kHotMax), dim3(64), 0, hs, a);
-        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
+        hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 1>), g, dim3(64), 0, hs, a);
+        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 3>), g, dim3(192), 0, hs2, a);
     } else {
-        hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 1>), dim3(kHotMax), dim3(64), 0, hs, a);
-        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 3>), dim3(kHotMax), dim3(192), 0, hs2, a);
+        hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 1>), g, dim3(64), 0, hs, a);
+        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 3>), g, dim3(192), 0, hs2, a);
     }
     return hipGetLastError();
 }

@@ -40,7 +40,8 @@ struct BatchCtl {
     unsigned long long table_bytes;// state-table bytes read + written by the region stage
     uint32_t n_normal;         // records in the normal partition: pass 0 routes the previous
                                // batch's hot regions to bins of their own (k_route_ranges)
-    uint32_t pad1;
+    uint32_t n_hot;            // hot regions of the batch (k_hot_prep): the next batches'
+                               // chain-launch size hint (RegionArgs::chain_grid)
 };
 // A region holding more than kGrowUsed live keys after a batch (or one that overflowed)
 // flags its limiter for growth (rl_engine doubles its region count at the next status
@@ -137,6 +138,9 @@ struct RegionArgs {
     uint32_t chain_split;      // (set by the launcher) 1: single-wave chains take every region;
                                // 2: two-key regions go to the 3-wave launch
     uint32_t chain3;           // rl_tune("chain3"): two-key regions as 3-wave workgroups
+    uint32_t chain_grid;       // workgroups of the chain launches (each loops over the hot list
+                               // with that stride): sized on the host from an earlier batch's
+                               // hot count, so a batch with no hot region launches few idle ones
     // routed hot regions (hot_list entries with kHotRoutedBit): region, first record, count
     const uint32_t* route_list;
     const uint32_t* route_start;

@@ -276,8 +276,9 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             const int64_t x = __shfl_xor(wmin, o, 64);
             wmin = x < wmin ? x : wmin;
         }
-        int64_t wi = slot >= 0 ? (geo.curr_start - wmin) / L.window_ms : 3;
-        if (wi > 3) wi = 3;
+        // (window starts are multiples of w: compares instead of a 64-bit division)
+        const int64_t dw = geo.curr_start - wmin, w1 = L.window_ms;
+        const int64_t wi = slot < 0 ? 3 : dw == 0 ? 0 : dw == w1 ? 1 : dw == 2 * w1 ? 2 : 3;
         const uint64_t b0 = __ballot(wi & 1), b1 = __ballot(wi & 2);
         same_w = ((wi & 1) ? b0 : ~b0) & ((wi & 2) ? b1 : ~b1);
         elig_m = __ballot(slot >= 0 && wi < 3 && q.op == (uint32_t)kOpAcquire);

@@ -288,3 +288,27 @@ def test_hot_routed_device_entry_ragged():
         ga.append(a.cpu().numpy()); gr.append(r.cpu().numpy())
     want = COracle(lims).run(*tr[:4])
     assert_same((np.concatenate(ga), np.concatenate(gr), None), want, "routed device ragged")
+
+
+@pytest.mark.parametrize("chain3", [0, 1])
+def test_hot_chain_launch_smaller_than_hot_list(chain3):
+    # the chain launch is sized from an earlier batch's hot count (RegionArgs::chain_grid):
+    # batch 1 has no hot region (next launch: 64 workgroups), batch 2 makes the largest
+    # 1024+ regions hot, so each chain workgroup loops over many hot-list entries
+    lims = [[rl_amd.SW, 100, 60000, 0.0], [rl_amd.TB, 50, 60000, 10.0]]
+    tr = hot_trace(31, 600_000, 20_000, 0.2, [0, 1], 60_000, hot_keys=3)
+    e = rl_amd.Engine(max_batch=1 << 22, capacity=1 << 14)
+    for l in lims:
+        e.add_limiter(*l)
+    e.tune("chain3", chain3)
+    o = COracle(lims)
+    cut = 200_000
+    got = [[], [], []]
+    for b, sl in enumerate((slice(0, cut), slice(cut, None))):
+        if b == 1:
+            e.tune("hot_threshold", 1)
+        a, r, t, st = e.execute(*(x[sl] for x in tr))
+        assert st == rl_amd.RL_OK, rl_amd.strerror(st)
+        got[0].append(a); got[1].append(r); got[2].append(t)
+    want = o.run(*tr)
+    assert_same(tuple(np.concatenate(g) for g in got), want, f"chain grid {chain3}")
