@@ -165,6 +165,7 @@ struct rl_engine {
     uint32_t ablate = 0;                    // rl_tune("ablate"), measurement only
     int bin_shift = 0;                      // rl_tune("bin_shift"): 0 or 3 (regions per bin 1/8)
     uint32_t up_per_cu = 0, sc_per_cu = 0, un_per_cu = 0;   // rl_tune("*_per_cu"), 0 = default
+    uint32_t sc_split = 1;                  // rl_tune("scatter_split"): k_scatter_split
     bool force_wide = false;                // rl_tune("wide_records"): 32-B records (any time span)
     bool auto_grow = true;                  // !RL_OPT_FIXED_CAPACITY
     uint64_t grows = 0;                     // region-count doublings done (rl_batch_stats)
@@ -657,12 +658,11 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = B.d_ctl;
     pa.counts = B.counts; pa.bin_base = B.bin_base; pa.ablate = e->ablate;
     pa.bin_shift = bsh;
-    pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu;
+    pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu; pa.sc_split = e->sc_split;
     // ---- pass 0 (low digit) from the caller's arrays; routed hot regions get bins
     // 2^d0 + slot and their records go straight to the final array (rec1)
     pa.digit_shift = 0; pa.digit_bits = route ? ceil_log2(nb0) : d0;
     pa.n_bins_pass = nb0;
-    pa.region_count = nullptr;
     pa.rec_out = B.rec0; pa.pos_out = B.pos0;
     if (route) {
         pa.route_list = e->route_list; pa.lo_bins = 1u << d0; pa.rec_out_route = B.rec1;
@@ -1041,6 +1041,7 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "ablate") == 0) { e->ablate = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "upsweep_per_cu") == 0) { e->up_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "scatter_per_cu") == 0) { e->sc_per_cu = (uint32_t)value; return RL_OK; }
+    if (std::strcmp(key, "scatter_split") == 0) { e->sc_split = value != 0; return RL_OK; }
     if (std::strcmp(key, "unpermute_per_cu") == 0) { e->un_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "debug_regions") == 0) { e->debug_regions = value != 0; return RL_OK; }
     if (std::strcmp(key, "wide_records") == 0) { e->force_wide = value != 0; return RL_OK; }

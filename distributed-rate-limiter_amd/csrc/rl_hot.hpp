@@ -363,7 +363,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         return;
     }
     const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
+    RL_GLOBAL Slot* tab = as_global((Slot*)L.table + (size_t)(region - L.region_base) * NS);
     if (wid == 0) {
         // ---- load + rebuild the region (as k_regions), find or insert the hot key's slot
         Slot img[NS / 64];

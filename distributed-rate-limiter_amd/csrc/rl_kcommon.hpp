@@ -43,6 +43,18 @@ __device__ inline uint32_t xcd_remap(uint32_t b, uint32_t n) {
     return base + b / 8;
 }
 
+// A pointer read from memory (the state tables in DevLimiter) is a generic one: its loads and
+// stores become flat instructions, which count against both vmcnt and lgkmcnt, so every wait
+// around them — LDS waits included — turns into a full drain. Table accesses go through
+// global-address-space pointers instead.
+#ifdef __HIP_DEVICE_COMPILE__
+#define RL_GLOBAL __attribute__((address_space(1)))
+#else
+#define RL_GLOBAL                       // (the host pass parses device code only)
+#endif
+template <class T>
+__device__ inline RL_GLOBAL T* as_global(T* p) { return (RL_GLOBAL T*)p; }
+
 __device__ inline uint32_t popc_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

@@ -72,9 +72,9 @@ struct PartArgs {
     int32_t bin_shift;         // bin = region >> bin_shift (0: one region per bin, 3: eight)
     uint32_t up_per_cu;        // persistent-grid workgroups per CU (0: default)
     uint32_t sc_per_cu;
+    uint32_t sc_split;         // rl_tune("scatter_split"): loads and stores in separate waves
     uint32_t* counts;          // [bins][n_tiles]: per-tile histogram, then exclusive row scan
     const uint32_t* bin_base;  // [bins]
-    uint32_t* region_count;    // nullable: full-region histogram (multi-pass only)
     BatchCtl* ctl;
     uint32_t ablate;           // rl_tune("ablate"): measurement-only variants (0 = product)
     uint32_t n_bins_pass;      // bins of this pass (0: 1 << digit_bits)

@@ -7,7 +7,8 @@
 namespace rl {
 
 // ------------------------------------------------------------------ 1. upsweep
-template <class Codec, bool RAW>
+// DIG: the pass stores each element's digit for the scatter (routing).
+template <class Codec, bool RAW, bool DIG>
 __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
     // dynamic LDS (upsweep_lds_bytes): the histogram of this pass's bins, then the route table
     // when routing; sized to the pass so that 4 workgroups fit a CU at 8192 bins
@@ -48,8 +49,7 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
                     const uint32_t g = bin_of<Codec, RAW>(a, i, L);
                     const uint32_t d = pass_digit(a, g, R);
                     atomicAdd(&hist[d], 1u);
-                    if (RAW && a.digit) a.digit[i] = (uint16_t)d;     // the scatter reads it back
-                    if (a.region_count) atomicAdd(&a.region_count[g], 1u);
+                    if constexpr (DIG) a.digit[i] = (uint16_t)d;      // the scatter reads it back
                 }
             }
         }
@@ -117,14 +117,24 @@ struct ScatterIn;
 template <class Codec>
 struct ScatterIn<Codec, true> {
     uint64_t key; int64_t now_ns; int32_t permits; uint32_t lim; uint32_t op; uint32_t dig;
+    // Every load is unconditional (an absent array reads the key's bytes instead and the
+    // value is dropped): a load under a branch leaves the wait-count pass unsure how many
+    // loads are in flight, and it then waits for all of them — the whole prefetch ring and
+    // every store before it — at the first use of any input.
     __device__ inline void load(const PartArgs& a, uint32_t i) {
         key = ld<kNtScIn>(a.key + i);
         now_ns = ld<kNtScIn>(a.now_ns + i);
         permits = ld<kNtScIn>(a.permits + i);
-        lim = a.limiter ? a.limiter[i] : 0u;
-        op = a.op ? a.op[i] : 0u;
-        dig = a.digit ? ld<kNtScIn>(a.digit + i) : 0u;
+        const uint16_t* lp = a.limiter ? a.limiter + i : (const uint16_t*)(a.key + i);
+        const uint8_t* op_p = a.op ? a.op + i : (const uint8_t*)(a.key + i);
+        const uint16_t* dp = a.digit ? a.digit + i : (const uint16_t*)(a.key + i);
+        lim = *lp;            // raw: masked where used (a select here would wait for it)
+        op = *op_p;
+        dig = ld<kNtScIn>(dp);
     }
+    __device__ inline uint32_t lim_v(const PartArgs& a) const { return a.limiter ? lim : 0u; }
+    __device__ inline uint32_t op_v(const PartArgs& a) const { return a.op ? op : 0u; }
+    __device__ inline uint32_t dig_v(const PartArgs& a) const { return a.digit ? dig : 0u; }
 };
 
 template <class Codec>
@@ -134,6 +144,20 @@ struct ScatterIn<Codec, false> {
         rec = ((const typename Codec::Rec*)a.rec_in)[i];
     }
 };
+
+// The record output arrays: routed regions' records go straight to the final array, at a
+// uniform element offset from the normal one. Selecting between the two kernel-argument
+// pointers per lane let the compiler fold their reads into one vector load from the argument
+// segment at a lane-chosen offset, followed by a vmcnt(0) wait in every round (a drain of the
+// prefetched loads and of every store in flight); a pointer rebuilt from integers is a flat
+// one, whose stores the wait-count pass cannot track either. An offset keeps both out.
+template <class Rec>
+__device__ inline void scatter_outputs(const PartArgs& a, Rec*& out_norm, int64_t& route_off,
+                                       uint32_t& lo_route) {
+    out_norm = (Rec*)a.rec_out;
+    route_off = a.route_list ? (Rec*)a.rec_out_route - out_norm : 0;
+    lo_route = a.route_list ? a.lo_bins : 0xFFFFFFFFu;
+}
 
 #ifndef RL_SCATTER_DEPTH
 #define RL_SCATTER_DEPTH 8
@@ -162,6 +186,10 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     // it store to the padding past the whole batch (a.n), clear of the routed records
     const uint32_t n = a.n_dev ? *a.n_dev : a.n;
     const uint32_t last = n - 1;
+    Rec* out_norm;
+    int64_t route_off;
+    uint32_t lo_route;
+    scatter_outputs(a, out_norm, route_off, lo_route);
     uint64_t mn = ~0ULL, mx = 0;
     bool overflow = false;
     for (uint32_t it = 0;; ++it) {
@@ -187,7 +215,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
             uint32_t d = 0;
             if (active) {
                 if constexpr (RAW) {
-                    uint32_t lim = in.lim, op = in.op;
+                    uint32_t lim = in.lim_v(a), op = in.op_v(a);
                     const int32_t p = in.permits;
                     const int64_t now_ms = floor_div_ms(in.now_ns);
                     const bool lim_ok = lim < a.n_lim;
@@ -208,7 +236,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                         mx = k > mx ? k : mx;
                     }
                     // routing: the upsweep's digit (route-table lookup done once per request)
-                    d = a.digit ? (uint32_t)in.dig
+                    d = a.digit ? in.dig_v(a)
                                 : (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
                                    >> a.digit_shift) & ((1u << a.digit_bits) - 1);
                 } else {
@@ -241,8 +269,8 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
             uint32_t wpos = active ? pos : a.n + t;
             if (abl & kAblSeqRecStore) wpos = active ? i : a.n + t;
             // a routed region's records go straight to the final record array
-            Rec* dst = (Rec*)(a.route_list && active && d >= a.lo_bins ? a.rec_out_route : a.rec_out);
-            if (!(abl & kAblNoRecStore)) st_rec<kNtScRec>(dst + wpos, rec);
+            Rec* dst = out_norm + ((active && d >= lo_route ? route_off : 0) + wpos);
+            if (!(abl & kAblNoRecStore)) st_rec<kNtScRec>(dst, rec);
             if (!(abl & kAblNoPosStore)) st<kNtScPos>(a.pos_out + (active ? i : a.n + t), pos);
         };
         // Unrolled by the prefetch depth so the input registers rotate without moves (a
@@ -269,6 +297,182 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
         const bool any_over = __syncthreads_or(overflow);
         if (t == 0) {
             for (int w = 1; w < kTileThreads / 64; ++w) {
+                mn = s_mm[0][w] < mn ? s_mm[0][w] : mn;
+                mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
+            }
+            if (mn != ~0ULL) atomicMin((unsigned long long*)&a.ctl->min_now_key, (unsigned long long)mn);
+            if (mx != 0) atomicMax((unsigned long long*)&a.ctl->max_now_key, (unsigned long long)mx);
+            if (any_over) atomicOr(&a.ctl->span_overflow, 1u);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 3b. split scatter
+// The same stable partition with the global loads and the stores in different waves. gfx950
+// has one vmcnt for vector loads and stores, retired in issue order: in k_scatter a wave's
+// wait for its prefetched inputs also waits for the acks of every scattered record store it
+// issued before them (no-store ablation on sw_zipf: scatter0 4.8 -> 2.8 ms). Here loader waves
+// (threads kTileThreads..2*kTileThreads-1) keep kSplitDepth rounds of inputs in flight,
+// encode each round and stage its records and digits in LDS one round ahead; the ranking
+// waves (threads 0..kTileThreads-1) read them from LDS, rank, and store — they issue no
+// global load inside a tile, so nothing ever waits behind their stores.
+#ifndef RL_SPLIT_DEPTH
+#define RL_SPLIT_DEPTH 4
+#endif
+constexpr int kSplitDepth = RL_SPLIT_DEPTH;       // loader rounds in flight (divides kTileItems)
+template <class Codec>
+__host__ __device__ inline size_t split_stage_off(uint32_t bins) {     // in u64 words, 16-B aligned
+    return ((size_t)bins + (bins + 1) / 2 + 1) & ~(size_t)1;
+}
+template <class Codec, bool RAW>
+__global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) {
+    using Rec = typename Codec::Rec;
+    constexpr int kRecV = (int)(sizeof(Rec) / 16);
+    static_assert(sizeof(Rec) % 16 == 0, "records are whole 16-B vectors");
+    extern __shared__ uint64_t dyn_lds64[];
+    __shared__ LimLds L;
+    __shared__ uint64_t s_mm[2][2 * kTileThreads / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const bool loader = t >= (uint32_t)kTileThreads;          // (wave-uniform)
+    const uint32_t lt = loader ? t - (uint32_t)kTileThreads : t;   // element within a round
+    const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
+    uint64_t* cntw = dyn_lds64;                               // as k_scatter
+    uint32_t* cur = (uint32_t*)(dyn_lds64 + bins);
+    Rec* stg = (Rec*)(dyn_lds64 + split_stage_off<Codec>(bins));   // [2][kTileThreads]
+    uint16_t* sdg = (uint16_t*)(stg + 2 * kTileThreads);           // [2][kTileThreads]
+    load_lim_lds(L, a);
+    int64_t base = 0;
+    if constexpr (RAW) base = a.ctl->base_ms;
+    const uint32_t n = a.n_dev ? *a.n_dev : a.n;
+    const uint32_t last = n - 1;
+    Rec* out_norm;
+    int64_t route_off;
+    uint32_t lo_route;
+    scatter_outputs(a, out_norm, route_off, lo_route);
+    uint64_t mn = ~0ULL, mx = 0;
+    bool overflow = false;
+    // (loaders) element i's record and digit, as k_scatter's round
+    auto encode = [&](const ScatterIn<Codec, RAW>& in, uint32_t i, Rec& rec, uint32_t& d) __attribute__((always_inline)) {
+        rec = Rec{};
+        d = 0;
+        if (i >= n) return;
+        if constexpr (RAW) {
+            uint32_t lim = in.lim_v(a), op = in.op_v(a);
+            const int32_t p = in.permits;
+            const int64_t now_ms = floor_div_ms(in.now_ns);
+            const bool lim_ok = lim < a.n_lim;
+            if (!lim_ok) lim = 0;
+            const bool invalid = !lim_ok || op > 2u || (op == 0u && p <= 0);
+            if (op > 2u) op = 0;
+            const uint64_t h = mix64(in.key);
+            rec = Codec::enc(h, now_ms, base, p, op, lim, invalid);
+            if (!invalid) {
+                const int64_t rel = now_ms - base;
+                if constexpr (std::is_same<Codec, CodecC>::value)
+                    overflow |= rel < 0 || rel > 0xFFFFFFFFLL;
+                const uint64_t k = ord_key(now_ms);
+                mn = k < mn ? k : mn;
+                mx = k > mx ? k : mx;
+            }
+            d = a.digit ? in.dig_v(a)
+                        : (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                           >> a.digit_shift) & ((1u << a.digit_bits) - 1);
+        } else {
+            rec = in.rec;
+            const uint32_t lim = Codec::limiter_of(rec);
+            d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                 >> a.digit_shift) & ((1u << a.digit_bits) - 1);
+        }
+    };
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t tile = tile_at(it, a.n_tiles);
+        if (tile >= a.n_tiles) break;
+        const uint32_t tile0 = tile * (uint32_t)kTile;
+        if (tile0 >= n) continue;                        // (workgroup-uniform)
+        __syncthreads();     // previous tile's LDS users are done
+        // The two roles run separate loops with the same barriers (1 + 2 per round), so the
+        // wait-count pass sees only the loaders' loads on one path and only the rankers'
+        // stores on the other. Round r: rankers take round r from stage r & 1 while loaders
+        // stage round r + 1 from the register ring (slot (r + 1) % depth) and reload that slot
+        // with round r + 1 + depth (past the tile: the next tile's inputs, or element n - 1).
+        if (loader) {
+            ScatterIn<Codec, RAW> in[kSplitDepth];
+            for (uint32_t b = lt; b < bins; b += kTileThreads)
+                cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
+#pragma unroll
+            for (int k = 0; k < kSplitDepth; ++k) in[k].load(a, min(tile0 + (uint32_t)k * kTileThreads + lt, last));
+            Rec r0;
+            uint32_t d0;
+            encode(in[0], tile0 + lt, r0, d0);           // round 0 staged before the loop
+            stg[lt] = r0;
+            sdg[lt] = (uint16_t)d0;
+            in[0].load(a, min(tile0 + (uint32_t)kSplitDepth * kTileThreads + lt, last));
+            __syncthreads();
+            auto stage = [&](int r, ScatterIn<Codec, RAW>& nxt) __attribute__((always_inline)) {
+                // (the last round stages the next tile's first, unread: that tile's prologue
+                // writes stage 0 again after its first barrier)
+                const uint32_t i = tile0 + (uint32_t)(r + 1) * kTileThreads + lt;
+                Rec nr;
+                uint32_t nd;
+                encode(nxt, i, nr, nd);
+                const uint32_t sl = (uint32_t)((r + 1) & 1) * kTileThreads + lt;
+                stg[sl] = nr;
+                sdg[sl] = (uint16_t)nd;
+                nxt.load(a, min(i + (uint32_t)kSplitDepth * kTileThreads, last));
+                __syncthreads();
+                __syncthreads();
+            };
+            for (int r = 0; r < kTileItems; r += kSplitDepth) {
+#pragma unroll
+                for (int k = 0; k < kSplitDepth; ++k) stage(r + k, in[(k + 1) % kSplitDepth]);
+            }
+        } else {
+            for (uint32_t b = lt; b < bins; b += kTileThreads) cntw[b] = 0;
+            __syncthreads();
+            for (int r = 0; r < kTileItems; ++r) {
+                const uint32_t i = tile0 + (uint32_t)r * kTileThreads + lt;
+                const bool active = i < n;
+                const uint32_t sl = (uint32_t)(r & 1) * kTileThreads + lt;
+                u32x4_t rv[kRecV];                        // the record, kept in registers
+#pragma unroll
+                for (int k = 0; k < kRecV; ++k) rv[k] = ((const u32x4_t*)stg)[sl * kRecV + k];
+                const uint32_t d = sdg[sl];
+                const uint64_t m = wave_match(d, a.digit_bits, active);
+                const uint32_t lr = popc_below(m);
+                const uint32_t cnt = (uint32_t)__popcll(m);
+                const bool leader = active && lr == 0;
+                if (leader) ((uint8_t*)&cntw[d])[wid] = (uint8_t)cnt;
+                __syncthreads();
+                uint32_t pos = 0;
+                if (active) {
+                    const uint64_t below = wid == 0 ? 0ULL : cntw[d] & ((1ULL << (8 * wid)) - 1);
+                    pos = cur[d] + lr + __builtin_amdgcn_sad_u8((uint32_t)below, 0u, 0u) +
+                          __builtin_amdgcn_sad_u8((uint32_t)(below >> 32), 0u, 0u);
+                }
+                __syncthreads();
+                if (leader) {
+                    atomicAdd(&cur[d], cnt);
+                    ((uint8_t*)&cntw[d])[wid] = 0;
+                }
+                const uint32_t wpos = active ? pos : a.n + lt;
+                Rec* dst = out_norm + ((active && d >= lo_route ? route_off : 0) + wpos);
+#pragma unroll
+                for (int k = 0; k < kRecV; ++k) ((u32x4_t*)dst)[k] = rv[k];
+                st<kNtScPos>(a.pos_out + (active ? i : a.n + lt), pos);
+            }
+        }
+    }
+    if constexpr (RAW) {
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a1 = __shfl_xor(mn, o, 64), b1 = __shfl_xor(mx, o, 64);
+            mn = a1 < mn ? a1 : mn;
+            mx = b1 > mx ? b1 : mx;
+        }
+        __syncthreads();
+        if (lane == 0) { s_mm[0][wid] = mn; s_mm[1][wid] = mx; }
+        const bool any_over = __syncthreads_or(overflow);
+        if (t == 0) {
+            for (int w = 1; w < 2 * kTileThreads / 64; ++w) {
                 mn = s_mm[0][w] < mn ? s_mm[0][w] : mn;
                 mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
             }
@@ -495,12 +699,15 @@ hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s)
     const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
     if (bins > (1u << kMaxDigitBits)) return hipErrorInvalidValue;
     const size_t lds = bins * sizeof(uint32_t) + (a.route_list ? sizeof(RouteLds) : 0);
-    if (raw) {
-        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((k_upsweep<CodecC, true>), grid, block, lds, s, a);
+    if (raw && a.digit) {
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, true, true>), grid, block, lds, s, a);
+    } else if (raw) {
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, true, false>), grid, block, lds, s, a);
     } else {
-        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, false>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((k_upsweep<CodecC, false>), grid, block, lds, s, a);
+        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, false, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_upsweep<CodecC, false, false>), grid, block, lds, s, a);
     }
     return hipGetLastError();
 }
@@ -509,6 +716,19 @@ hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s)
     dim3 grid(persistent_grid(a.n_tiles, a.sc_per_cu ? a.sc_per_cu : 1)), block(kTileThreads);
     const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
     if (bins > (1u << kMaxDigitBits)) return hipErrorInvalidValue;
+    if (a.sc_split && !a.ablate) {
+        const dim3 b2(2 * kTileThreads);
+        const size_t lc = split_stage_off<CodecC>(bins) * 8 + 2 * kTileThreads * (sizeof(RecC) + 2);
+        const size_t lw = split_stage_off<CodecW>(bins) * 8 + 2 * kTileThreads * (sizeof(RecW) + 2);
+        if (raw) {
+            if (wide) hipLaunchKernelGGL((k_scatter_split<CodecW, true>), grid, b2, lw, s, a);
+            else hipLaunchKernelGGL((k_scatter_split<CodecC, true>), grid, b2, lc, s, a);
+        } else {
+            if (wide) hipLaunchKernelGGL((k_scatter_split<CodecW, false>), grid, b2, lw, s, a);
+            else hipLaunchKernelGGL((k_scatter_split<CodecC, false>), grid, b2, lc, s, a);
+        }
+        return hipGetLastError();
+    }
     const size_t lds = bins * (sizeof(uint64_t) + sizeof(uint32_t));
     if (raw) {
         if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, lds, s, a);

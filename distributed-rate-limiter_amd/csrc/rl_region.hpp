@@ -54,8 +54,8 @@ constexpr bool kSparseOn = !RL_NO_SPARSE;
 // probe that reaches such a bucket faults it in from HBM (128 B, + 32 B of cache words);
 // dead slots come in as tombstones. tab == nullptr: the whole image is in LDS.
 struct SparseSrc {
-    const Slot* tab;
-    const uint64_t* xtab;             // local-cache words (nullable)
+    const RL_GLOBAL Slot* tab;
+    const RL_GLOBAL uint64_t* xtab;   // local-cache words (nullable)
     int64_t keep;                     // slot_live threshold (keep_from)
     bool long_chain;                  // per lane: a probe went past two used buckets
 };
@@ -554,10 +554,10 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
 
     // ---- load the region, dropping entries no request of this batch can see, and
     // rebuild its open-addressing table (no tombstones ever reach HBM)
-    Slot* tab = (Slot*)L.table + (size_t)(region - L.region_base) * NS;
-    uint64_t* xtab = nullptr;                       // the slots' local-cache states
+    RL_GLOBAL Slot* tab = as_global((Slot*)L.table + (size_t)(region - L.region_base) * NS);
+    RL_GLOBAL uint64_t* xtab = nullptr;             // the slots' local-cache states
     if constexpr (LdsT::kCache)
-        if (L.cache_table) xtab = (uint64_t*)L.cache_table + (size_t)(region - L.region_base) * NS;
+        if (L.cache_table) xtab = as_global((uint64_t*)L.cache_table + (size_t)(region - L.region_base) * NS);
     // Few records: probe and update single buckets in HBM (128 B read + 32 B written per
     // distinct key) instead of moving the 8 KB image both ways.
     const bool sparse = kSparseOn && RPB == 1 && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
