@@ -232,6 +232,7 @@ struct UnpermArgs {
     uint32_t n_tiles;
     uint32_t ablate;
     uint32_t per_cu;           // persistent-grid workgroups per CU (0: default)
+    uint32_t split;            // rl_tune("unpermute_split"): gathers and stores in separate waves
 };
 
 struct SynthArgs {

@@ -650,6 +650,84 @@ __global__ __launch_bounds__(kTileThreads) void k_unpermute(UnpermArgs a) {
   }
 }
 
+// Split unpermute (rl_tune unpermute_split): the position reads and result gathers in loader
+// waves (threads kTileThreads..), the decision stores in storer waves, one round apart through
+// LDS, so that no wait for a gather sits behind the acks of earlier stores (one vmcnt for both
+// on gfx950). Loaders keep kUnPosDepth rounds of positions and kUnGatherDepth rounds of
+// gathers in flight. One-array batches only (no pos1 pass, no tokens): k_unpermute otherwise.
+constexpr int kUnPosDepth = 8, kUnGatherDepth = 4;
+template <class Res>
+__global__ __launch_bounds__(2 * kTileThreads) void k_unpermute_split(UnpermArgs a) {
+    __shared__ Res stage[2][kTileThreads];
+    const uint32_t t = threadIdx.x;
+    const bool loader = t >= (uint32_t)kTileThreads;          // (wave-uniform)
+    const uint32_t lt = loader ? t - (uint32_t)kTileThreads : t;
+    const Res* __restrict__ res = (const Res*)a.res;
+    const Res* __restrict__ res_hi = (const Res*)a.res_hi;
+    const uint32_t nn = res_hi ? a.ctl->n_normal : 0u;
+    const uint32_t last = a.n - 1;
+    for (uint32_t it = 0;; ++it) {
+        const uint32_t tile = tile_at(it, a.n_tiles);
+        if (tile >= a.n_tiles) break;
+        const uint32_t tbase = tile * (uint32_t)kTile + lt;
+        __syncthreads();                                      // last tile's stage readers are done
+        if (loader) {
+            uint32_t P[kUnPosDepth];
+            Res V[kUnGatherDepth];
+            auto pos_of = [&](int r) { return ld<kNtUn>(a.pos0 + min(tbase + (uint32_t)r * kTileThreads, last)); };
+            auto gather = [&](uint32_t p) { return (res_hi && p >= nn ? res_hi : res)[p]; };
+#pragma unroll
+            for (int k = 0; k < kUnPosDepth; ++k) P[k] = pos_of(k);
+#pragma unroll
+            for (int k = 0; k < kUnGatherDepth; ++k) {
+                V[k] = gather(P[k]);
+                P[k] = pos_of(k + kUnPosDepth);
+            }
+            // round r: stage round r's results; gather round r + G (its position, slot
+            // (r + G) % D, arrived); reload that slot with round r + G + D
+            for (int r0 = 0; r0 < kTileItems; r0 += kUnPosDepth) {
+#pragma unroll
+                for (int k = 0; k < kUnPosDepth; ++k) {
+                    const int r = r0 + k;
+                    stage[r & 1][lt] = V[k % kUnGatherDepth];
+                    V[k % kUnGatherDepth] = gather(P[(k + kUnGatherDepth) % kUnPosDepth]);
+                    P[(k + kUnGatherDepth) % kUnPosDepth] = pos_of(r + kUnGatherDepth + kUnPosDepth);
+                    __syncthreads();
+                }
+            }
+        } else {
+            for (int r = 0; r < kTileItems; ++r) {
+                __syncthreads();
+                const Res v = stage[r & 1][lt];
+                const uint32_t i = tbase + (uint32_t)r * kTileThreads;
+                if (i < a.n) {
+                    st<kNtUn>(a.allowed + i, (uint8_t)(v & 1u));
+                    st<kNtUn>(a.remaining + i, (int64_t)(v >> 1) - kResBias);
+                }
+            }
+        }
+    }
+    if (!loader && a.ctl && a.ctl->n_esc != 0) {
+        // as k_unpermute: the escape code decoded as (allowed 1, remaining -3) is rewritten
+        // from the side array by the thread that stored it
+        const Res* rf = (const Res*)a.res_final;
+        for (uint32_t it = 0;; ++it) {
+            const uint32_t tile = tile_at(it, a.n_tiles);
+            if (tile >= a.n_tiles) break;
+            for (int r = 0; r < kTileItems; ++r) {
+                const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+                if (i >= a.n) break;
+                uint32_t j = a.pos0[i];
+                if (a.pos1_final && j < a.ctl->n_normal) j = a.pos1_final[j];
+                if ((uint64_t)rf[j] == kResEscape) {
+                    a.allowed[i] = 0;
+                    a.remaining[i] = a.ext[j];
+                }
+            }
+        }
+    }
+}
+
 // Two-pass batches: undo the high-digit pass first. mid[j] = res[pos1[j]] for j in
 // pass-0 order: pos1 is read in order and, since pass 0 left the records sorted by low
 // digit, consecutive j fall into one low-digit run whose elements go to the 2^d1
@@ -825,6 +903,14 @@ hipError_t launch_unpermute(const UnpermArgs& a_in, int res_bytes, hipStream_t s
         a.pos1 = nullptr;
     }
     dim3 g(persistent_grid(a.n_tiles, a.per_cu ? a.per_cu : 1)), b(kTileThreads);
+    if (a.split && !a.pos1 && !a.tokens_out && !a.ablate) {
+        const dim3 b2(2 * kTileThreads);
+        if (res_bytes == 8) hipLaunchKernelGGL(k_unpermute_split<uint64_t>, g, b2, 0, s, a);
+        else if (res_bytes == 1) hipLaunchKernelGGL(k_unpermute_split<uint8_t>, g, b2, 0, s, a);
+        else if (res_bytes == 2) hipLaunchKernelGGL(k_unpermute_split<uint16_t>, g, b2, 0, s, a);
+        else hipLaunchKernelGGL(k_unpermute_split<uint32_t>, g, b2, 0, s, a);
+        return hipGetLastError();
+    }
     if (res_bytes == 8) hipLaunchKernelGGL(k_unpermute<uint64_t>, g, b, 0, s, a);
     else if (res_bytes == 1) hipLaunchKernelGGL(k_unpermute<uint8_t>, g, b, 0, s, a);
     else if (res_bytes == 2) hipLaunchKernelGGL(k_unpermute<uint16_t>, g, b, 0, s, a);
