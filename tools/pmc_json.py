@@ -22,13 +22,16 @@ import os
 
 
 def stage_of(name: str):
+    def raw(n):  # second template argument: pass 0 reads the raw request arrays
+        args = n.split("<", 1)[1].split(">")[0].split(",")
+        return len(args) > 1 and args[1].strip() == "true"
     if "k_upsweep<" in name:
-        return "upsweep0" if name.rstrip(")").split(">")[0].endswith("true") else "upsweep1"
-    if "k_scatter<" in name:
-        return "scatter0" if name.rstrip(")").split(">")[0].endswith("true") else "scatter1"
+        return "upsweep0" if raw(name) else "upsweep1"
+    if "k_scatter<" in name or "k_scatter_split<" in name:
+        return "scatter0" if raw(name) else "scatter1"
     if "k_regions<" in name:
         return "region"
-    if "k_unpermute<" in name:
+    if "k_unpermute<" in name or "k_unpermute_split<" in name:
         return "unpermute"
     return None
 
