@@ -234,6 +234,15 @@ __device__ inline uint64_t wave_max64(uint64_t v) {
     return v;
 }
 
+__device__ inline uint32_t wave_min32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) { const uint32_t x = __shfl_xor(v, o, 64); v = x < v ? x : v; }
+    return v;
+}
+__device__ inline uint32_t wave_max32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) { const uint32_t x = __shfl_xor(v, o, 64); v = x > v ? x : v; }
+    return v;
+}
+
 template <class Codec>
 __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
     using Rec = typename Codec::Rec;
@@ -274,8 +283,19 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
                 const bool rest = valid && !hot0 && (k == 0 || !hot1);
                 uint64_t mn = ~0ULL, mx = 0ULL;
                 if (k == 0 || two) {                      // (wave-uniform)
-                    mn = wave_min64(plain ? ord_key(q.now_ms) : ~0ULL);
-                    mx = wave_max64(plain ? ord_key(q.now_ms) : 0ULL);
+                    if constexpr (std::is_same<Codec, CodecC>::value) {
+                        // compact records: now = base + now_rel, so the 32-bit offsets order
+                        // the same way and the reductions move half the bits
+                        const uint32_t m32 = wave_min32(plain ? r.now_rel : ~0u);
+                        const uint32_t x32 = wave_max32(plain ? r.now_rel : 0u);
+                        if (__ballot(plain)) {
+                            mn = ord_key(base + (int64_t)m32);
+                            mx = ord_key(base + (int64_t)x32);
+                        }
+                    } else {
+                        mn = wave_min64(plain ? ord_key(q.now_ms) : ~0ULL);
+                        mx = wave_max64(plain ? ord_key(q.now_ms) : 0ULL);
+                    }
                 }
                 const uint32_t ns = (uint32_t)__popcll(__ballot(special));
                 const uint32_t nh = (uint32_t)__popcll(__ballot(hot));

@@ -1,10 +1,11 @@
 #!/bin/bash
-# router capacity error: the two owners' engines fed directly, in two concurrent processes
+# 32-bit time reductions in k_hot_summ: hot/config/parity GPU tests, kernel trace of sw_zipf
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u tools/repro_router_cap.py mixed_tenants 0 > gpurun_out/repro0.log 2>&1 &
-p0=$!
-timeout -k 10 400 python -u tools/repro_router_cap.py mixed_tenants 1 > gpurun_out/repro1.log 2>&1
-r1=$?
-wait $p0; r0=$?
-echo "rc $r0 $r1"; grep owner gpurun_out/repro0.log gpurun_out/repro1.log
+true
+true
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_j -o trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra > gpurun_out/prof_j.log 2>&1 || { tail -5 gpurun_out/prof_j.log; exit 1; }
+f=$(find gpurun_out/prof_j -name "*kernel_stats.csv" | head -1)
+grep -E "k_hot_summ|k_scatter_split|k_unpermute" $f | cut -c1-160
+echo done
