@@ -9,8 +9,10 @@ and time moves forward exactly as in a replay.
 Default workload (N=1): BASELINE.json configs[2], the largest single-GPU configuration —
 sliding window 1000/min (SlidingWindowRateLimiter.java:158-180), 100M keys Zipf s=1.1,
 256M-request batches spanning 60 s each. The same JSON line carries configs[1] (token
-bucket cap 50 at 10/s, 1M keys uniform, 64M-request batches; `tb_uniform`) and configs[0]
-(the reference's single-key benchmark; `config1`) as extra keys, each parity-checked.
+bucket cap 50 at 10/s, 1M keys uniform, 64M-request batches; `tb_uniform`), the per-GPU
+share of configs[4] (TB 50@10/s + SW 1000/min, Zipf s=1.1, 125M keys, 2^27 requests per
+step; `zipf_1b`) and configs[0] (the reference's single-key benchmark; `config1`) as extra
+keys, each with its own roofline, CPU baseline and parity check.
 
 Multi-GPU (torchrun, one rank per GPU): weak scaling. Every rank is a front-end that
 receives its own slice of the global stream; requests are routed to the owner shard
@@ -424,7 +426,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="requests per GPU per step (override)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
-                    help="N=1: skip the extra tb_uniform / config1 keys of the line")
+                    help="N=1: skip the extra tb_uniform / zipf_1b / config1 keys of the line")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--tune", action="append", default=[],
                     help="engine knob key=value (rl_tune), e.g. bin_shift=0")
@@ -470,18 +472,22 @@ def main():
     del in0
     if baseline and not args.no_extra:
         torch.cuda.empty_cache()
-        if args.config != "tb_uniform":
-            # BASELINE configs[1] on the same box: the token-bucket line, parity incl. balances
-            tb, tin0, tkeep0 = run("tb_uniform", args, 1, 0, local, dev, False, args.steps,
+        # BASELINE configs[1] (tb_uniform) and the per-GPU share of configs[4] (zipf_1b: the
+        # north-star 1B-key TB + SW trace at 8 GPUs) on the same box, each with its own
+        # roofline, CPU baseline and batch-0 parity (TB balances bit-for-bit)
+        for extra in ("tb_uniform", "zipf_1b"):
+            if extra == args.config:
+                continue
+            xo, xin0, xkeep0 = run(extra, args, 1, 0, local, dev, False, args.steps,
                                    args.warmup, parity_tokens=True)
-            cbt, dec_t, bal_t, mt = cpu_baseline(CONFIGS["tb_uniform"], *tin0, args.cpu_sample,
-                                                 tkeep0[0], tkeep0[1], tkeep0[2], single_thread=False)
-            out["tb_uniform"] = {k: tb[k] for k in ("value", "unit", "ms_per_step", "config", "stage_ms",
-                                                    "batch_stats", "status")}
-            out["tb_uniform"]["roofline_frac"] = tb["roofline"]["frac"]
-            out["tb_uniform"]["cpu_baseline"] = cbt
-            out["tb_uniform"]["parity"] = parity_text(dec_t, bal_t, mt)
-            del tin0
+            cbx, dec_x, bal_x, mx = cpu_baseline(CONFIGS[extra], *xin0, args.cpu_sample,
+                                                 xkeep0[0], xkeep0[1], xkeep0[2], single_thread=False)
+            out[extra] = {k: xo[k] for k in ("value", "unit", "ms_per_step", "config", "stage_ms",
+                                             "batch_stats", "status", "roofline")}
+            out[extra]["roofline_frac"] = xo["roofline"]["frac"]
+            out[extra]["cpu_baseline"] = cbx
+            out[extra]["parity"] = parity_text(dec_x, bal_x, mx)
+            del xin0, xkeep0
             torch.cuda.empty_cache()
         out["config1"] = config1_line(dev)
     if rank == 0:

@@ -1011,6 +1011,8 @@ extern "C" int rl_batch_stats_get(rl_engine* e, rl_batch_stats* out) {
     out->table_bytes = c.table_bytes;
     out->cache_hits = c.cache_hits;
     out->table_grows = e->grows;
+    out->hot_regions = c.n_hot;
+    out->routed = e->last_n >= c.n_normal ? e->last_n - c.n_normal : 0;
     return RL_OK;
 }
 

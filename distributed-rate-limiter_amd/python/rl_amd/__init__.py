@@ -85,7 +85,8 @@ class LimiterConfig(ctypes.Structure):
 class BatchStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("n", "allowed", "distinct_keys", "invalid",
                                                  "capacity_errors", "regions_touched",
-                                                 "table_bytes", "cache_hits", "table_grows")]
+                                                 "table_bytes", "cache_hits", "table_grows",
+                                                 "hot_regions", "routed")]
 
 
 class TraceSpec(ctypes.Structure):

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 2
+#define RL_ABI_VERSION 3
 
 /* ---- status codes -------------------------------------------------------- */
 #define RL_OK                   0
@@ -145,6 +145,9 @@ typedef struct rl_batch_stats {
     uint64_t cache_hits;        /* SW local-cache rejections (ratelimiter.cache.hits,
                                    SlidingWindowRateLimiter.java:75-77,96)                  */
     uint64_t table_grows;       /* region-count doublings so far (on-demand table growth)   */
+    uint64_t hot_regions;       /* regions decided by the hot-key chains in the last batch   */
+    uint64_t routed;            /* requests of the last batch routed straight to their final
+                                   partition in pass 0 (the previous batch's hot regions)    */
 } rl_batch_stats;
 
 /* Create / destroy an engine on one GPU. Replaces the JedisPool + Redis keyspace

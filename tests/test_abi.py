@@ -38,7 +38,7 @@ def test_rccl_transport_library_exports():
 
 def test_abi_version_and_strerror():
     L = rl_amd.lib()
-    assert L.rl_abi_version() == 2
+    assert L.rl_abi_version() == 3
     assert rl_amd.strerror(0) == "ok"
     assert "capacity" in rl_amd.strerror(rl_amd.RL_E_CAPACITY) or "full" in rl_amd.strerror(-3)
 

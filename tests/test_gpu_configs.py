@@ -10,7 +10,12 @@ remaining bit-exactly with the C oracle (key-sharded over 16 host threads):
   10 limiters with TB + SW, 1-byte and 2-byte results;
 * zipf_1b (configs[4]): TB(50, 10/s) + SW(1000/min), 16M requests in 2 batches;
 * sw_zipf (configs[2]): ONE full 256M-request batch, so the hot chain of its top region
-  (~29.8M records) is compared end to end, not a prefix;
+  (~29.8M records) is compared end to end, not a prefix; and three consecutive whole
+  batches, so the routed steady state (pass 0 routes the previous batch's hot regions)
+  is compared too;
+* the steady state of configs[3]/[4]: six (mixed_tenants) and four (zipf_1b) consecutive
+  whole bench batches, each compared with a persistent oracle right after it runs, and one
+  whole zipf_1b batch with its TB balances;
 * config 1 (configs[0], RateLimiterBenchmark.java:48-71): the single-key SW 100000/min
   stream of 100,000 tryAcquire("user123"), as one batch and as 100 batches.
 """
@@ -100,6 +105,95 @@ def run_config(name, n, batches, pipeline=False, cuts=None, cfg=None, tune=()):
     o.close()
     assert_same(got, want, name)
     return k, got, st
+
+
+def run_stream(name, batches, n=None, tune=(), timing=False):
+    """Consecutive whole bench batches (bench.py steps 0 .. batches-1 of a default run:
+    same generator, index base and time axis), each compared with a persistent C oracle
+    right after it runs, so the engine's state after many batches — the steady state the
+    bench's numbers come from — is checked, not just a prefix of batch 0. Returns the
+    per-batch engine stats (and stage times with `timing`)."""
+    cfgs, t0_ns = bench_configs()
+    cfg = cfgs[name]
+    n = n or cfg["batch"]
+    has_tb = any(l[0] == rl_amd.TB for l in cfg["limiters"])
+    eng = rl_amd.Engine(device=0, max_batch=n, capacity=cfg["capacity"], stage_timing=timing)
+    for l in cfg["limiters"]:
+        eng.add_limiter(*l)
+    for k, v in tune:
+        eng.tune(k, v)
+    o = COracle(cfg["limiters"], nthreads=ORACLE_THREADS)
+    dev = torch.device("cuda", 0)
+    allowed = torch.empty(n, dtype=torch.uint8, device=dev)
+    remaining = torch.empty(n, dtype=torch.int64, device=dev)
+    tokens = torch.empty(n, dtype=torch.float64, device=dev) if has_tb else None
+    out = []
+    for b in range(batches):
+        keys, permits, now, lim = synth(eng, cfg, t0_ns, n, index_base=b * cfg["batch"])
+        torch.cuda.synchronize()
+        eng.execute_device(n, keys, permits, now, lim, None, allowed, remaining, tokens)
+        st = eng.last_status()
+        assert st == rl_amd.RL_OK, f"{name} batch {b}: {rl_amd.strerror(st)}"
+        stats = eng.stats()
+        if timing:
+            stats["stage_ms"] = eng.stage_times()
+        got = (allowed.cpu().numpy(), remaining.cpu().numpy(),
+               None if tokens is None else tokens.cpu().numpy())
+        k = keys.cpu().numpy().view(np.uint64)
+        li = None if lim is None else lim.cpu().numpy().view(np.uint16)
+        want = o.run(k, permits.cpu().numpy(), now.cpu().numpy(), li, None, want_tokens=has_tb)
+        del keys, permits, now, lim
+        if has_tb:
+            assert np.isfinite(want[2]).sum() > 0
+        assert_same(got, want, f"{name} batch {b}")
+        assert 0 < got[0].sum() < n
+        print(f"{name} batch {b}: {int(got[0].sum())} allowed, hot regions {stats['hot_regions']}, "
+              f"routed {stats['routed']}"
+              + (f", region stage {stats['stage_ms'].get('region', -1):.2f} ms" if timing else ""),
+              flush=True)
+        out.append(stats)
+    eng.close()
+    o.close()
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_config_mixed_tenants_steady_state():
+    """configs[3]'s per-GPU share for six consecutive 2^27-request bench batches (6 minutes of
+    trace time): from batch ~3 on, the SW perSecond(100) limiter's hot key lets one request
+    through every ~10 ms as its previous bucket's weight decays (SlidingWindowRateLimiter.java:
+    170-174), so its hot chain re-derives the denied interval [T0, T1) thousands of times per
+    batch — the regime that bounds the config's step time, compared request by request."""
+    stats = run_stream("mixed_tenants", 6, timing=True)
+    assert all(s["hot_regions"] > 0 for s in stats)
+
+
+@pytest.mark.timeout(400)
+def test_config_zipf_1b_full_batch():
+    """configs[4]'s per-GPU share, one whole 2^27-request bench batch (TB + SW, Zipf over
+    125M keys), decisions, remaining and TB balances bit-for-bit."""
+    cfgs, _ = bench_configs()
+    n = cfgs["zipf_1b"]["batch"]
+    k, got, st = run_config("zipf_1b", n, 1)
+    assert st["hot_regions"] > 0
+    assert np.isfinite(got[2]).sum() > n // 4
+
+
+@pytest.mark.timeout(600)
+def test_config_sw_zipf_routed_batches():
+    """configs[2] (the headline) as three consecutive whole 2^28-request bench batches: from
+    batch 1 on, pass 0 routes the previous batch's hot regions straight to their final bins
+    (hot-region routing), which is the regime every timed bench step runs in."""
+    stats = run_stream("sw_zipf", 3)
+    assert stats[0]["routed"] == 0
+    assert all(s["routed"] > (1 << 26) for s in stats[1:]), [s["routed"] for s in stats]
+
+
+@pytest.mark.timeout(600)
+def test_config_zipf_1b_steady_state():
+    """configs[4]'s per-GPU share over four consecutive whole bench batches (routing on)."""
+    stats = run_stream("zipf_1b", 4)
+    assert all(s["routed"] > 0 for s in stats[1:])
 
 
 def test_config_mixed_tenants_16m():
