@@ -270,9 +270,12 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
     total_steps = steps + warm
     # weak scaling: each shard owns 1/ws of the keys but sees ws x n requests' worth of
     # key space across ranks, i.e. the same number of requests per GPU; a shard's table
-    # is sized for its share of the global key population. An owner can receive up to
-    # ws x n requests in a skewed step.
-    eng = rl_amd.Engine(device=local, max_batch=n * ws,
+    # is sized for its share of the global key population. The C-ABI router's owner decides
+    # at most its receive capacity (min(ws, 2) x n) per exchange round and splits a step
+    # into rounds when an owner receives more (a skewed step); the python router hands an
+    # owner everything it receives (up to ws x n).
+    cap = n * ws if (ws > 1 and args.router == "python") else n * min(ws, 2)
+    eng = rl_amd.Engine(device=local, max_batch=cap,
                         capacity=cfg["capacity"] * ws * args.table_scale, stage_timing=False,
                         shard_index=rank, shard_count=ws,
                         pipeline=ws == 1 and args.pipeline)
@@ -304,7 +307,7 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
         else:
             from rl_amd.capi_router import CRouter
             router = CRouter(eng, ws, rank, n, transport="host" if rehearse else "rccl",
-                             device=local)
+                             device=local, recv_cap=args.recv_cap)
             if cfg["dist"] == rl_amd.DIST_ZIPF and not args.no_directory:
                 directory = plan_directory(router, cfg, inputs, n)
 
@@ -411,6 +414,12 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
                                               "capacity_errors", "regions_touched")},
         "status": rl_amd.strerror(st),
     }
+    if router is not None and hasattr(router, "stats"):
+        rs = router.stats()
+        out["router"] = {"rounds_per_step": rs["rounds"] / max(1, rs["steps"]),
+                         "split_steps": rs["split_steps"], "max_recv": rs["max_recv"],
+                         "recv_cap": rs["recv_cap"], "reserved_gb": rs["reserved_bytes"] / 1e9,
+                         "header_sync_ms_per_step": rs["header_sync_ns"] * 1e-6 / max(1, rs["steps"])}
     if router is not None and hasattr(router, "close"):
         router.close()
     eng.close()
@@ -439,6 +448,8 @@ def main():
                     help="also record hipEvents inside the timed steps (diagnostics only)")
     ap.add_argument("--router", choices=("capi", "python"), default="capi",
                     help="N>1: the C-ABI router (product path) or the torch.distributed one")
+    ap.add_argument("--recv-cap", type=int, default=0,
+                    help="N>1: requests an owner decides per exchange round (0: min(N, 2) x batch)")
     ap.add_argument("--no-directory", action="store_true",
                     help="N>1: hash owners only (no hot-key directory on Zipf configs)")
     args = ap.parse_args()

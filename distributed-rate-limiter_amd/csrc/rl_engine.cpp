@@ -170,6 +170,7 @@ struct rl_engine {
                                             // 0 off, 1 on, 2 two-pass batches (measured faster there)
     bool force_wide = false;                // rl_tune("wide_records"): 32-B records (any time span)
     bool auto_grow = true;                  // !RL_OPT_FIXED_CAPACITY
+    uint32_t inject_fail = 0;               // rl_tune("fail_batches"): tests of callers' error paths
     uint64_t grows = 0;                     // region-count doublings done (rl_batch_stats)
 };
 
@@ -500,7 +501,10 @@ extern "C" int rl_limiter_slots(rl_engine* e, uint16_t limiter, uint64_t* slots)
 
 static int ensure_scratch(rl_engine* e, BatchScratch& B, size_t n, bool wide, uint32_t bins, uint32_t n_tiles) {
     if (n > B.cap_n || (wide && !B.cap_wide)) {
-        size_t cap = std::max<size_t>(n, std::min<size_t>(e->opts.max_batch, std::max<size_t>(n, 1u << 20)));
+        // sized for this batch (+1/8 headroom), not max_batch: a router's engine accepts up
+        // to its receive capacity but usually sees about its per-rank share
+        size_t cap = std::max<size_t>(n, std::min<size_t>(e->opts.max_batch,
+                                                          std::max<size_t>(n + n / 8, 1u << 20)));
         const size_t rb = wide ? sizeof(RecW) : sizeof(RecC);
         const size_t padn = cap + kTileThreads;   // kernels write inactive lanes past n
         dfree(B.rec0); dfree(B.rec1); dfree(B.pos0); dfree(B.pos1); dfree(B.res); dfree(B.tok);
@@ -521,7 +525,7 @@ static int ensure_scratch(rl_engine* e, BatchScratch& B, size_t n, bool wide, ui
     if (need_counts > B.counts_cap) {
         dfree(B.counts);
         size_t c = std::max(need_counts, (size_t)(1u << kMaxDigitBits) *
-                                              ((std::max<size_t>(n, e->opts.max_batch) + kTile - 1) / kTile));
+                                              ((std::max<size_t>(n, B.cap_n) + kTile - 1) / kTile));
         if (dalloc(&B.counts, c) != RL_OK) return RL_E_NOMEM;
         B.counts_cap = c;
     }
@@ -578,6 +582,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     e->last_status = RL_OK;
     if (n == 0) return RL_OK;
     if (!key || !permits || !now_ns || !allowed || !remaining) return RL_E_INVALID_ARG;
+    if (e->inject_fail) { --e->inject_fail; return RL_E_DEVICE; }   // nothing enqueued
     hipStream_t s = e->stream;
     if (e->lims.empty()) {
         HIP_OK(launch_fill_invalid(allowed, remaining, tokens_after, (uint32_t)n, s));
@@ -1094,6 +1099,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
         e->split_hot = value != 0;
         return RL_OK;
     }
+    if (std::strcmp(key, "fail_batches") == 0) {      // the next `value` batches fail (RL_E_DEVICE)
+        if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
+        e->inject_fail = (uint32_t)value;
+        return RL_OK;
+    }
     if (std::strcmp(key, "bin_shift") == 0) {
         if (value != 0 && value != kBinShift) return RL_E_INVALID_ARG;
         e->bin_shift = (int)value;
@@ -1244,6 +1254,7 @@ int route_pack_wire_mm(rl_engine* e, size_t n, const uint32_t* perm, const uint6
     return RL_OK;
 }
 int engine_device(rl_engine* e) { return e ? e->device : 0; }
+size_t engine_max_batch(rl_engine* e) { return e ? (size_t)e->opts.max_batch : 0; }
 }  // namespace rl
 
 extern "C" int rl_route_unwire(rl_engine* e, size_t m, const uint64_t* wire, uint32_t n_src,

@@ -383,10 +383,13 @@ hipError_t launch_route_unpack_ret(uint32_t n, const uint32_t* perm, const void*
                                    hipStream_t s);
 hipError_t launch_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride,
                                    hipStream_t s);
-// Router header: kHdrWords int64 per peer row.
-constexpr uint32_t kHdrWords = 8;
+// Router header: kHdrWords int64 per peer row: kHdrFixed fixed words, then the source's
+// request count for every owner (so every rank knows the whole count matrix).
+constexpr uint32_t kHdrFixed = 8;
+constexpr uint32_t kHdrWords = kHdrFixed + kMaxShards;
 hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, int64_t cap,
-                              uint32_t g, const uint64_t* part, uint32_t nparts, hipStream_t s);
+                              int64_t rcap, uint32_t g, const uint64_t* part, uint32_t nparts,
+                              hipStream_t s);
 hipError_t launch_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, int64_t rem,
                              hipStream_t s);
 
@@ -396,5 +399,6 @@ int route_pack_wire_mm(rl_engine* e, size_t n, const uint32_t* perm, const uint6
                        uint64_t* wire_out, uint16_t* limiter_out, int64_t* hdr, uint64_t* part,
                        uint32_t* nparts, void* stream);
 int engine_device(rl_engine* e);
+size_t engine_max_batch(rl_engine* e);
 
 }  // namespace rl

@@ -394,11 +394,13 @@ __global__ void k_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* 
 }
 
 // Router header rows (kHdrWords int64 each): {count (already there), base_ms, overflow,
-// published status, capacity, min now_ms, max now_ms, 0}; min / max folded from
+// published status, capacity, min now_ms, max now_ms, receive capacity} and then this
+// source's count for every owner (column 0 of every row); min / max folded from
 // k_route_pack_wire's per-block partials (nparts = 0: an empty batch, min > max).
 __global__ __launch_bounds__(256) void k_fill_header(int64_t* hdr, const int64_t* base_ovf,
-                                                     int64_t status, int64_t cap, uint32_t g,
-                                                     const uint64_t* part, uint32_t nparts) {
+                                                     int64_t status, int64_t cap, int64_t rcap,
+                                                     uint32_t g, const uint64_t* part,
+                                                     uint32_t nparts) {
     __shared__ uint64_t s_mm[2][4];
     const uint32_t t = threadIdx.x;
     uint64_t mn = ~0ULL, mx = 0;
@@ -425,14 +427,16 @@ __global__ __launch_bounds__(256) void k_fill_header(int64_t* hdr, const int64_t
         row[4] = cap;
         row[5] = mn == ~0ULL ? INT64_MAX : (int64_t)(mn ^ 0x8000000000000000ULL);
         row[6] = mx == 0ULL ? INT64_MIN : (int64_t)(mx ^ 0x8000000000000000ULL);
-        row[7] = 0;
+        row[7] = rcap;
+        for (uint32_t q = 0; q < g; ++q) row[kHdrFixed + q] = hdr[(size_t)q * kHdrWords];
     }
 }
 
 hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t status, int64_t cap,
-                              uint32_t g, const uint64_t* part, uint32_t nparts, hipStream_t s) {
-    hipLaunchKernelGGL(k_fill_header, dim3(1), dim3(256), 0, s, hdr, base_ovf, status, cap, g, part,
-                       nparts);
+                              int64_t rcap, uint32_t g, const uint64_t* part, uint32_t nparts,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(k_fill_header, dim3(1), dim3(256), 0, s, hdr, base_ovf, status, cap, rcap, g,
+                       part, nparts);
     return hipGetLastError();
 }
 

@@ -48,7 +48,7 @@ EXPORTS = [
     "rl_route_unpack_return", "rl_route_partition_device", "rl_set_owner_directory",
     "rl_owner_of_engine", "rl_router_create", "rl_router_step", "rl_router_finish",
     "rl_router_plan_directory", "rl_router_destroy", "rl_pin_host", "rl_unpin_host",
-    "rl_grow_limiter", "rl_limiter_slots",
+    "rl_grow_limiter", "rl_limiter_slots", "rl_router_create_ex", "rl_router_stats_get",
 ]
 RCCL_EXPORTS = ["rl_rccl_unique_id", "rl_transport_rccl_create", "rl_transport_rccl_destroy"]
 STATE_SW_BUCKET, STATE_TB_BUCKET = 0, 1

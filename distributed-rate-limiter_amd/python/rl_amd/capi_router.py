@@ -103,11 +103,23 @@ class HostTransport:
             return -1
 
 
+class RouterOpts(ctypes.Structure):
+    _fields_ = [("max_batch", ctypes.c_size_t), ("recv_cap", ctypes.c_size_t)]
+
+
+class RouterStats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in ("steps", "rounds", "split_steps", "max_recv",
+                                               "header_sync_ns", "recv_cap", "reserved_bytes")]
+
+
 class CRouter:
-    """rl_router_create / step / finish / plan_directory / destroy over one engine."""
+    """rl_router_create_ex / step / finish / plan_directory / stats / destroy over one engine.
+    recv_cap: requests the owner's engine decides per exchange round (0: min(world, 2) x
+    max_batch, clamped to the engine's max_batch); a step in which an owner receives more
+    is split into rounds by every rank alike."""
 
     def __init__(self, eng: "rl_amd.Engine", world: int, rank: int, max_batch: int,
-                 transport: str = "rccl", device: int = 0, group=None):
+                 transport: str = "rccl", device: int = 0, group=None, recv_cap: int = 0):
         self._L = rl_amd.lib()
         self.world, self.rank = world, rank
         self.t = Transport()
@@ -133,9 +145,10 @@ class CRouter:
             raise ValueError(transport)
         vp = ctypes.c_void_p
         L = self._L
-        L.rl_router_create.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32,
-                                       ctypes.POINTER(Transport), ctypes.c_size_t,
-                                       ctypes.POINTER(vp)]
+        L.rl_router_create_ex.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.POINTER(Transport), ctypes.POINTER(RouterOpts),
+                                          ctypes.POINTER(vp)]
+        L.rl_router_stats_get.argtypes = [vp, ctypes.POINTER(RouterStats)]
         L.rl_router_step.argtypes = [vp, ctypes.c_size_t] + [vp] * 7
         L.rl_router_finish.argtypes = [vp]
         L.rl_router_plan_directory.argtypes = [vp, ctypes.c_size_t, vp, vp, ctypes.c_uint64,
@@ -143,10 +156,11 @@ class CRouter:
         L.rl_router_destroy.argtypes = [vp]
         L.rl_router_destroy.restype = None
         h = vp()
-        st = L.rl_router_create(eng.handle, world, rank, ctypes.byref(self.t), max_batch,
-                                ctypes.byref(h))
+        o = RouterOpts(max_batch, recv_cap)
+        st = L.rl_router_create_ex(eng.handle, world, rank, ctypes.byref(self.t), ctypes.byref(o),
+                                   ctypes.byref(h))
         if st != rl_amd.RL_OK:
-            raise rl_amd.RlError(st, "rl_router_create")
+            raise rl_amd.RlError(st, "rl_router_create_ex")
         self._h = h
 
     def step(self, n, keys, permits, now_ns, limiter, allowed, remaining, stream=None):
@@ -175,6 +189,11 @@ class CRouter:
         if st != rl_amd.RL_OK:
             raise rl_amd.RlError(st, "rl_router_plan_directory")
         return placed.value
+
+    def stats(self) -> dict:
+        st = RouterStats()
+        self._L.rl_router_stats_get(self._h, ctypes.byref(st))
+        return {f: getattr(st, f) for f, _ in RouterStats._fields_}
 
     def close(self):
         if getattr(self, "_h", None):

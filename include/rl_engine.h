@@ -227,7 +227,8 @@ int  rl_sync(rl_engine* e);
  * tables: the previous batch's hot regions skip the second partition pass, default 1),
  * "region_order" (largest regions dispatched first, default 1), "sparse_max", "split_hot",
  * "region_walk", "bin_shift", "stage_timing", "debug_regions" and the "*_per_cu" grid
- * sizes. Every setting gives the same decisions. */
+ * sizes. Every setting gives the same decisions. "fail_batches" = k makes the next k batch
+ * calls fail with RL_E_DEVICE before enqueuing anything (tests of callers' error paths). */
 int  rl_tune(rl_engine* e, const char* key, int64_t value);
 /* Diagnostics (not needed by callers). "region_times": after a batch run with
  * rl_tune("debug_regions", 1), copies per-bin {t_start, t_end, records, rounds,
@@ -380,10 +381,31 @@ typedef struct rl_transport {
 } rl_transport;
 
 typedef struct rl_router rl_router;
-/* max_batch: the largest per-rank n of rl_router_step (an owner may receive up to
- * world x max_batch; its engine must accept that: rl_opts.max_batch). */
+typedef struct rl_router_opts {
+    size_t max_batch;           /* the largest per-rank n of rl_router_step                    */
+    size_t recv_cap;            /* requests an owner decides per exchange round; 0 = min(world,
+                                   2) x max_batch; clamped to the engine's rl_opts.max_batch. A
+                                   step in which some owner receives more runs in several
+                                   rounds (every rank derives the same plan from the header)   */
+} rl_router_opts;
+/* Every device buffer a step uses is reserved here (send side ~50 B x max_batch, receive
+ * side ~56 B x recv_cap, the return trip, the directory exchange), so a step never
+ * allocates between two collectives. rl_router_create = _ex with recv_cap 0. */
+int  rl_router_create_ex(rl_engine* e, uint32_t world, uint32_t rank, const rl_transport* t,
+                         const rl_router_opts* opts, rl_router** out);
 int  rl_router_create(rl_engine* e, uint32_t world, uint32_t rank, const rl_transport* t,
                       size_t max_batch, rl_router** out);
+typedef struct rl_router_stats {
+    uint64_t steps;             /* rl_router_step calls that reached the header exchange       */
+    uint64_t rounds;            /* exchange rounds (== steps unless a step was split)          */
+    uint64_t split_steps;       /* steps in which some owner received more than recv_cap       */
+    uint64_t max_recv;          /* most requests this rank's engine received in one step       */
+    uint64_t header_sync_ns;    /* host time blocked on the per-step header read, summed (it
+                                   also waits for this rank's previous step to drain)          */
+    uint64_t recv_cap;
+    uint64_t reserved_bytes;    /* device bytes reserved by rl_router_create_ex                */
+} rl_router_stats;
+int  rl_router_stats_get(rl_router* r, rl_router_stats* out);
 /* tryAcquire over this rank's slice of the global arrival stream (device buffers; the
  * ranks' slices are ordered by rank). Same results as one engine on the concatenated
  * stream. One host synchronisation per step (the header exchange: RCCL takes its

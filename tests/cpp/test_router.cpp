@@ -4,7 +4,9 @@
 //   test_router loop : G = 2 and 4 routers (threads), each with its own engine shard, on the
 //                      box's one GPU, over an in-process loopback transport; compact and wide
 //                      layouts, token-bucket time regression (exception blocks), the hot-key
-//                      directory, and a collective error (a shard's region overflows)
+//                      directory, a collective error (a shard's region overflows), an
+//                      engine failure on one rank, steps split into rounds (an owner receives
+//                      more than its receive capacity), and what a router reserves
 //   test_router rccl : one rank over the RCCL transport (librl_rccl.so), world 1
 #include <hip/hip_runtime.h>
 
@@ -111,14 +113,18 @@ static int loop_a2av(void* ctx, const void* send, const uint64_t* so, const uint
     return rc;
 }
 
-struct Result { std::vector<uint8_t> a; std::vector<int64_t> r; int finish = 0; uint32_t placed = 0; int step_rc = 0; };
+struct Result {
+    std::vector<uint8_t> a; std::vector<int64_t> r; int finish = 0; uint32_t placed = 0; int step_rc = 0;
+    int fail_step = -1;               // first step whose rl_router_step returned an error
+    rl_router_stats st{};
+};
 
 static const int64_t kLims[2][3] = {{1, 50, 60000}, {0, 30, 5000}};   // TB 50 @ 10/s, SW 30 / 5 s
 static const double kRefill[2] = {10.0, 0.0};
 
 static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int steps, bool dir,
                      uint64_t capacity, Result* out, rl_transport* ext_t = nullptr,
-                     bool nosync_finish = false) {
+                     bool nosync_finish = false, size_t recv_cap = 0, int fail_at = -1) {
     HIPC(hipSetDevice(0));
     rl_opts o{};
     o.device = 0; o.max_batch = (uint64_t)G * n; o.default_capacity = capacity;
@@ -136,7 +142,9 @@ static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int
     rl_transport t{&lr, loop_a2av};
     if (ext_t) t = *ext_t;
     rl_router* r = nullptr;
-    CHECK(rl_router_create(e, (uint32_t)G, (uint32_t)rank, &t, n, &r) == RL_OK);
+    rl_router_opts ro{};
+    ro.max_batch = n; ro.recv_cap = recv_cap;
+    CHECK(rl_router_create_ex(e, (uint32_t)G, (uint32_t)rank, &t, &ro, &r) == RL_OK);
     hipStream_t s;
     HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     uint64_t* dk; int32_t* dp; int64_t* dt; uint16_t* dl; uint8_t* da; int64_t* dr;
@@ -162,8 +170,9 @@ static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int
         HIPC(hipMemcpyAsync(dp, &tr->permits[b], n * 4, hipMemcpyHostToDevice, s));
         HIPC(hipMemcpyAsync(dt, &tr->now[b], n * 8, hipMemcpyHostToDevice, s));
         HIPC(hipMemcpyAsync(dl, &tr->lim[b], n * 2, hipMemcpyHostToDevice, s));
+        if (st == fail_at) CHECK(rl_tune(e, "fail_batches", 1) == RL_OK);   // this rank's engine only
         const int rc = rl_router_step(r, n, dk, dp, dt, dl, da, dr, s);
-        if (rc != RL_OK && out->step_rc == RL_OK) out->step_rc = rc;
+        if (rc != RL_OK && out->step_rc == RL_OK) { out->step_rc = rc; out->fail_step = st; }
         // nosync_finish: the last step's work is still queued on s when finish is called
         // (finish must wait for it itself)
         if (nosync_finish && st == steps - 1) out->finish = rl_router_finish(r);
@@ -172,6 +181,7 @@ static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int
         HIPC(hipStreamSynchronize(s));
     }
     if (!nosync_finish) out->finish = rl_router_finish(r);
+    CHECK(rl_router_stats_get(r, &out->st) == RL_OK);
     rl_router_destroy(r);
     HIPC(hipFree(dk)); HIPC(hipFree(dp)); HIPC(hipFree(dt)); HIPC(hipFree(dl)); HIPC(hipFree(da)); HIPC(hipFree(dr));
     HIPC(hipStreamDestroy(s));
@@ -206,20 +216,89 @@ static void compare(const Trace& tr, int G, size_t n, int steps, const std::vect
 }
 
 static void loop_case(int G, size_t n, int steps, int64_t span_ms, bool regress, bool dir,
-                      const char* what) {
+                      const char* what, size_t recv_cap = 0) {
     Trace tr = make_trace((size_t)G * n * steps, 0xC0FFEE + G + (regress ? 7 : 0), span_ms, regress);
     Loop loop(G);
     std::vector<Result> res(G);
     std::vector<std::thread> th;
     for (int rank = 0; rank < G; ++rank)
-        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, dir, (uint64_t)1 << 16, &res[rank], nullptr, false);
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, dir, (uint64_t)1 << 16, &res[rank], nullptr,
+                        false, recv_cap, -1);
     for (auto& x : th) x.join();
     for (int rank = 0; rank < G; ++rank) {
         CHECK(res[rank].step_rc == RL_OK);
         CHECK(res[rank].finish == RL_OK);
+        CHECK(res[rank].st.steps == (uint64_t)steps);
         if (dir) CHECK(res[rank].placed == 16 && res[rank].placed == res[0].placed);
+        if (recv_cap) {                          // every step split into the same rounds everywhere
+            CHECK(res[rank].st.split_steps == (uint64_t)steps);
+            CHECK(res[rank].st.rounds == res[0].st.rounds && res[rank].st.rounds > (uint64_t)steps);
+            CHECK(res[rank].st.recv_cap == recv_cap);
+        } else {
+            CHECK(res[rank].st.split_steps == 0 && res[rank].st.rounds == (uint64_t)steps);
+        }
     }
     compare(tr, G, n, steps, res, what);
+    std::printf("  rounds %llu over %d steps, max received %llu, header sync %.3f ms/step\n",
+                (unsigned long long)res[0].st.rounds, steps, (unsigned long long)res[0].st.max_recv,
+                res[0].st.header_sync_ns * 1e-6 / steps);
+}
+
+// One rank's engine fails a batch (fail_batches, before anything is enqueued): that rank's
+// step leaves its requests undecided and publishes the error; EVERY rank's next step returns
+// it (the same status at the same step), and no rank hangs in a collective.
+static void loop_engine_fail_case() {
+    const int G = 4;
+    const size_t n = 30000;
+    const int steps = 4, fail_rank = 2, fail_at = 1;
+    Trace tr = make_trace((size_t)G * n * steps, 0xFA11, 30000, false);
+    Loop loop(G);
+    std::vector<Result> res(G);
+    std::vector<std::thread> th;
+    for (int rank = 0; rank < G; ++rank)
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1 << 16, &res[rank],
+                        nullptr, false, (size_t)0, rank == fail_rank ? fail_at : -1);
+    for (auto& x : th) x.join();
+    for (int rank = 0; rank < G; ++rank) {
+        CHECK(res[rank].step_rc == RL_E_DEVICE);
+        CHECK(res[rank].fail_step == fail_at + 1);
+        CHECK(res[rank].finish == RL_OK);            // reported once, at the step
+    }
+    std::printf("engine failure on rank %d at step %d: every rank's step %d returned %d %d %d %d\n",
+                fail_rank, fail_at, res[0].fail_step, res[0].step_rc, res[1].step_rc, res[2].step_rc,
+                res[3].step_rc);
+}
+
+// What a router reserves at creation: nothing proportional to world x max_batch (the receive
+// side is recv_cap, default min(world, 2) x max_batch; the return trip is sized for the
+// requests really exchanged, not world x max_batch per segment).
+static void reserve_case() {
+    const uint32_t G = 8;
+    const size_t n = (size_t)1 << 20;
+    rl_opts o{};
+    o.device = 0; o.max_batch = 2 * n; o.default_capacity = 1 << 16; o.shard_index = 0; o.shard_count = G;
+    rl_engine* e = nullptr;
+    CHECK(rl_create(&o, &e) == RL_OK);
+    rl_transport t{nullptr, [](void*, const void*, const uint64_t*, const uint64_t*, void*, const uint64_t*,
+                               const uint64_t*, void*) { return -1; }};
+    rl_router* r = nullptr;
+    CHECK(rl_router_create(e, G, 0, &t, n, &r) == RL_OK);
+    rl_router_stats st{};
+    CHECK(rl_router_stats_get(r, &st) == RL_OK);
+    CHECK(st.recv_cap == 2 * n);
+    const uint64_t fixed = 4u << 20;                       // headers, directory, exception blocks
+    CHECK(st.reserved_bytes <= 58 * (uint64_t)n + 65 * st.recv_cap + fixed);
+    CHECK(st.reserved_bytes < (uint64_t)G * n * 47);      // round 3 reserved ~(47 G + 8 G^2) x n
+    std::printf("router reserve: world %u, max_batch %zu -> recv_cap %llu, %.1f MB (%.1f B per request)\n",
+                G, n, (unsigned long long)st.recv_cap, st.reserved_bytes / 1e6, (double)st.reserved_bytes / n);
+    rl_router_destroy(r);
+    // an explicit receive capacity is clamped to what the engine accepts
+    rl_router_opts ro{};
+    ro.max_batch = n; ro.recv_cap = 16 * n;
+    CHECK(rl_router_create_ex(e, G, 0, &t, &ro, &r) == RL_OK);
+    CHECK(rl_router_stats_get(r, &st) == RL_OK && st.recv_cap == 2 * n);
+    rl_router_destroy(r);
+    rl_destroy(e);
 }
 
 // finish called right after the last step, with that step still queued on the caller's
@@ -234,7 +313,7 @@ static void loop_nosync_finish_case() {
     std::vector<std::thread> th;
     for (int rank = 0; rank < G; ++rank)
         th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1 << 16, &res[rank],
-                        nullptr, true);
+                        nullptr, true, (size_t)0, -1);
     for (auto& x : th) x.join();
     for (int rank = 0; rank < G; ++rank) CHECK(res[rank].step_rc == RL_OK && res[rank].finish == RL_OK);
     compare(tr, G, n, steps, res, "G=2 finish without a caller sync");
@@ -263,7 +342,7 @@ static void loop_span_case() {
     std::vector<std::thread> th;
     for (int rank = 0; rank < G; ++rank)
         th.emplace_back(run_rank, G, rank, &loop, &tr, n, 1, false, (uint64_t)1 << 14, &res[rank],
-                        nullptr, false);
+                        nullptr, false, (size_t)0, -1);
     for (auto& x : th) x.join();
     for (int rank = 0; rank < G; ++rank) CHECK(res[rank].step_rc == RL_OK && res[rank].finish == RL_OK);
     compare(tr, G, n, 1, res, "G=2 merged span > 2^31 ms (bases within 2^30)");
@@ -281,7 +360,8 @@ static void loop_error_case() {
     std::vector<Result> res(G);
     std::vector<std::thread> th;
     for (int rank = 0; rank < G; ++rank)
-        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1, &res[rank], nullptr, false);
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1, &res[rank], nullptr, false,
+                        (size_t)0, -1);
     for (auto& x : th) x.join();
     for (int rank = 0; rank < G; ++rank) {
         const bool failed = res[rank].step_rc == RL_E_CAPACITY || res[rank].finish == RL_E_CAPACITY;
@@ -300,6 +380,11 @@ int main(int argc, char** argv) {
         loop_case(2, 50000, 2, (int64_t)1 << 36, false, false, "G=2 wide (span > 2^32 ms)");
         loop_case(4, 50000, 3, 30000, true, false, "G=4 TB regression (exception blocks)");
         loop_case(4, 50000, 3, 30000, false, true, "G=4 hot-key directory");
+        loop_case(4, 50000, 3, 30000, false, false, "G=4 split rounds (recv_cap 20000)", 20000);
+        loop_case(2, 50000, 2, (int64_t)1 << 36, false, false, "G=2 wide + split rounds", 30001);
+        loop_case(4, 50000, 3, 30000, true, true, "G=4 directory + TB regression + split", 17777);
+        loop_engine_fail_case();
+        reserve_case();
         loop_nosync_finish_case();
         loop_span_case();
         loop_error_case();
