@@ -266,7 +266,8 @@ extern "C" int rl_router_step(rl_router* r, size_t n, const uint64_t* key, const
     // the previous batch is complete (ordered before the header exchange): its status is
     // published in the next header; the statuses received now (every rank's batch two steps
     // back) are the same on all ranks, so all fail together
-    if (r->pending) { r->pub = rl_last_status(e); r->pending = false; }
+    if (fatal(r->pub)) r->pub = RL_OK;              // delivered: every rank returns it now, once
+    if (r->pending) { r->pub = worse(r->pub, rl_last_status(e)); r->pending = false; }
     if (worst != RL_OK) return (int)worst;
     // every rank sees every rank's capacities: a mismatch fails all of them here, before
     // any payload (all ranks must derive the same exchange plan)
@@ -386,7 +387,7 @@ extern "C" int rl_router_finish(rl_router* r) {
     // the last step may still run on the caller's stream (its return all-to-all and the
     // unpack that counts lost remainders): complete it before reading anything
     if (r->stepped) R_OK(hipEventSynchronize(r->done));
-    if (r->pending) { r->pub = rl_last_status(r->e); r->pending = false; }
+    if (r->pending) { r->pub = worse(r->pub, rl_last_status(r->e)); r->pending = false; }
     uint32_t lost = 0;
     R_OK(hipMemcpy(&lost, r->lost, 4, hipMemcpyDeviceToHost));
     if (lost) R_OK(hipMemset(r->lost, 0, 4));        // counted once: the next steps start clean

@@ -410,7 +410,8 @@ int  rl_router_stats_get(rl_router* r, rl_router_stats* out);
  * ranks' slices are ordered by rank). Same results as one engine on the concatenated
  * stream. One host synchronisation per step (the header exchange: RCCL takes its
  * per-peer counts on the host). Errors are collective: an engine error on any rank is
- * returned by EVERY rank's step two steps later (or by rl_router_finish). */
+ * returned, once, by EVERY rank's step two steps later (or by rl_router_finish); the
+ * router then goes on (the failed batch's requests read RL_REMAINING_ERROR). */
 int  rl_router_step(rl_router* r, size_t n, const uint64_t* key_hash, const int32_t* permits,
                     const int64_t* now_ns, const uint16_t* limiter, uint8_t* allowed,
                     int64_t* remaining, void* stream);
