@@ -438,7 +438,7 @@ def main():
                     help="N=1: skip the extra tb_uniform / zipf_1b / config1 keys of the line")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--tune", action="append", default=[],
-                    help="engine knob key=value (rl_tune), e.g. bin_shift=0")
+                    help="engine knob key=value (rl_tune), e.g. hot_threshold=32768")
     ap.add_argument("--table-scale", type=int, default=1,
                     help="size the state tables for this many times the config's key count "
                          "(engine sizing: lower load, more and smaller regions)")

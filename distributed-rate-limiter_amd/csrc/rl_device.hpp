@@ -34,8 +34,8 @@ constexpr int64_t kRemError = -3;     // state-table region full
 // inside each XCD's 4 MB L2.
 constexpr int kRegionSlots = 256;                 // slots per region (load <= ~0.5)
 constexpr int kRegionBits = 8;
-constexpr int kRegionsPerBin = 8;                 // regions per bin (bin_shift = 3) ...
-constexpr int kBinShift = 3;                      // ... every limiter has >= 8 regions
+constexpr int kRegionsPerBin = 8;                 // every limiter has >= 8 regions ...
+constexpr int kBinShift = 3;                      // ... (2^kBinShift)
 constexpr int kRing = 128;                        // per-wave pending ring (< 64 + 64 entries)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 

@@ -96,12 +96,8 @@ struct rl_engine {
     bool pipeline = false;                  // RL_OPT_PIPELINE
     hipStream_t pstream = nullptr;          // partition stream (pipeline)
     hipEvent_t in_ev = nullptr;             // pipeline: inputs ready on e->stream
-    hipStream_t hstream = nullptr;          // hot chains beside the normal regions (one key)
-    hipStream_t hstream2 = nullptr;         // ... (two keys: 3-wave workgroups)
-    hipEvent_t hot_ev[3] = {};              // fork, joins of hstream / hstream2
-    bool split_hot = true;                  // rl_tune("split_hot"): 0 = one 2-wave launch
-    uint32_t region_walk = 0;               // rl_tune("region_walk"): persistent waves per CU
-    uint32_t* d_work = nullptr;             // its claim counters (8 x 64 B)
+    hipStream_t hstream = nullptr;          // hot chains beside the normal regions
+    hipEvent_t hot_ev[2] = {};              // fork, join of hstream
     // hot regions
     uint32_t* hot_list = nullptr;           // [kHotListWords]: list, k_hot_select's meta, totals
     HotInfo* hot_info = nullptr;            // [kHotMax]
@@ -118,8 +114,6 @@ struct rl_engine {
     bool route = true;                      // rl_tune("route")
     bool region_order = true;               // rl_tune("region_order"): largest regions dispatched first
     uint32_t order_prefix = 4096;           // rl_tune("order_prefix"): ... after this many of the smallest
-    bool chain3 = false;                    // rl_tune("chain3"): two-key hot regions as 3-wave workgroups
-                                            // (0: single waves run both keys' passes; measured faster)
     uint32_t* order = nullptr;              // [order_cap + 1]
     size_t order_cap = 0;
     uint32_t* order_meta = nullptr;         // [kOrderMeta]
@@ -163,7 +157,6 @@ struct rl_engine {
     int last_status = RL_OK;
     uint64_t last_n = 0;
     uint32_t ablate = 0;                    // rl_tune("ablate"), measurement only
-    int bin_shift = 0;                      // rl_tune("bin_shift"): 0 or 3 (regions per bin 1/8)
     uint32_t up_per_cu = 0, sc_per_cu = 0, un_per_cu = 0;   // rl_tune("*_per_cu"), 0 = default
     uint32_t sc_split = 1;                  // rl_tune("scatter_split"): k_scatter_split
     uint32_t un_split = 2;                  // rl_tune("unpermute_split"): k_unpermute_split
@@ -267,10 +260,8 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     int prio_least = 0, prio_greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
     if (hipStreamCreateWithPriority(&e->hstream, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
-        hipStreamCreateWithPriority(&e->hstream2, hipStreamNonBlocking, prio_greatest) != hipSuccess ||
         hipEventCreateWithFlags(&e->hot_ev[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->hot_ev[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->hot_ev[2], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&e->hot_ev[1], hipEventDisableTiming) != hipSuccess) {
         rl_destroy(e);
         return RL_E_DEVICE;
     }
@@ -295,7 +286,6 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
              hipEventCreateWithFlags(&B.freed, hipEventDisableTiming) != hipSuccess))
             rc = RL_E_DEVICE;
     }
-    if (rc == RL_OK) rc = dalloc(&e->d_work, 128);
     if (rc == RL_OK) rc = dalloc(&e->d_stats, (size_t)kStatSlots * kStWords);
     if (rc == RL_OK && hipMemset(e->d_stats, 0, (size_t)kStatSlots * kStWords * 8) != hipSuccess)
         rc = RL_E_DEVICE;
@@ -320,7 +310,6 @@ extern "C" void rl_destroy(rl_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->pstream) (void)hipStreamSynchronize(e->pstream);
     if (e->hstream) (void)hipStreamSynchronize(e->hstream);
-    if (e->hstream2) (void)hipStreamSynchronize(e->hstream2);
     for (auto& l : e->lims) { dfree(l.table); dfree(l.cache_table); }
     dfree(e->d_lims); dfree(e->d_region_lim);
     for (BatchScratch& B : e->sc) {
@@ -335,7 +324,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
     dfree(e->route_list); dfree(e->route_start); dfree(e->route_cnt);
     dfree(e->order); dfree(e->order_meta);
-    dfree(e->d_stats); dfree(e->d_work);
+    dfree(e->d_stats);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
     dfree(e->route_scratch); dfree(e->route_counts); dfree(e->d_dir);
@@ -347,7 +336,6 @@ extern "C" void rl_destroy(rl_engine* e) {
     if (e->pstream) (void)hipStreamDestroy(e->pstream);
     if (e->in_ev) (void)hipEventDestroy(e->in_ev);
     if (e->hstream) (void)hipStreamDestroy(e->hstream);
-    if (e->hstream2) (void)hipStreamDestroy(e->hstream2);
     for (hipEvent_t ev : e->hot_ev) if (ev) (void)hipEventDestroy(ev);
     delete e;
 }
@@ -599,15 +587,14 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     const uint32_t nt = (uint32_t)((n + kTile - 1) / kTile);
     bool cache = false;
     for (auto& l : e->lims) cache |= l.dev.cache_ttl_ms > 0;
-    const int bsh = cache ? 0 : e->bin_shift;        // the local-cache kernel is bin_shift 0
-    const uint32_t n_bins = e->n_regions >> bsh;
+    const uint32_t n_bins = e->n_regions;            // one partition bin per region
     const int bitsP = std::max(1, ceil_log2(n_bins));
     const int passes = bitsP <= kMaxDigitBits ? 1 : 2;
     if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
     const int d0 = passes == 1 ? bitsP : bitsP - bitsP / 2;
     const int d1 = bitsP - d0;
     // hot-region routing: pass 0 gets kRouteSlots bins beyond the 2^d0 low-digit ones
-    const bool hot_on = e->hot_threshold > 0 && !cache && e->bin_shift == 0;
+    const bool hot_on = e->hot_threshold > 0 && !cache;
     const bool route = hot_on && e->route && passes == 2 && !e->pipeline &&
                        (1u << d0) + kRouteSlots <= (1u << kMaxDigitBits);
     const uint32_t nb0 = route ? (1u << d0) + kRouteSlots : 1u << d0;
@@ -642,7 +629,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     // the hot-key path assumes that a denial never changes state; with a local cache a
     // denial may (it puts the estimate, SlidingWindowRateLimiter.java:106-108)
-    const bool hot = e->hot_threshold > 0 && bsh == 0 && !cache;
+    const bool hot = hot_on;
     // records per region for the hot path: scaled with the batch by default (measured per
     // config: sw_zipf best at 65536 for 2^28 requests, zipf_1b at 32768 for 2^27)
     const uint32_t hot_thr = e->hot_thr_auto ? std::max<uint32_t>(e->hot_threshold, (uint32_t)(n >> 12))
@@ -664,7 +651,6 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.n = (uint32_t)n; pa.n_tiles = nt; pa.n_lim = (uint32_t)e->lims.size();
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = B.d_ctl;
     pa.counts = B.counts; pa.bin_base = B.bin_base; pa.ablate = e->ablate;
-    pa.bin_shift = bsh;
     pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu; pa.sc_split = e->sc_split;
     // ---- pass 0 (low digit) from the caller's arrays; routed hot regions get bins
     // 2^d0 + slot and their records go straight to the final array (rec1)
@@ -715,7 +701,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         // them; no full read of the records)
         BoundsArgs ba{};
         ba.rec = rec_final; ba.n = (uint32_t)n; ba.n_lim = (uint32_t)e->lims.size();
-        ba.lims = e->d_lims; ba.shard_bits = e->shard_bits; ba.bin_shift = bsh;
+        ba.lims = e->d_lims; ba.shard_bits = e->shard_bits;
         ba.rstart = B.region_start; ba.rend = B.region_count;
         ba.hi_base = B.bin_base; ba.hi_total = B.bin_total;
         ba.n_bins = n_bins; ba.d0 = d0; ba.d1 = d1;
@@ -733,14 +719,11 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ra.region_lim = e->d_region_lim;
     ra.lims = e->d_lims; ra.res = B.res; ra.ext = B.ext; ra.tok = tokens_after ? B.tok : nullptr;
     ra.ctl = B.d_ctl; ra.n_regions = e->n_regions; ra.n_total = (uint32_t)n; ra.ablate = e->ablate;
-    ra.shard_bits = e->shard_bits; ra.bin_shift = bsh;
+    ra.shard_bits = e->shard_bits;
     ra.skew_ms = e->opts.max_skew_ms;
     ra.stats = e->d_stats;
-    ra.work = e->d_work;
-    ra.walk = e->region_walk;
     ra.cache = cache ? 1u : 0u;
-    ra.sparse_max = bsh == 0 ? e->sparse_max : 0u;
-    ra.chain3 = e->chain3 ? 1u : 0u;
+    ra.sparse_max = e->sparse_max;
     // chain launch size: twice the hot count of the last batch the host saw complete (a
     // hint only: the chains loop over the hot list with the grid's stride), the whole
     // kHotMax before any batch has completed
@@ -770,7 +753,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ra.route_list = e->route_list; ra.route_start = e->route_start; ra.route_cnt = e->route_cnt;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
     }
-    if (e->region_order && bsh == 0) {
+    if (e->region_order) {
         if (e->order_cap < n_bins) {
             dfree(e->order);
             if (dalloc(&e->order, (size_t)n_bins + 1) != RL_OK) { e->order_cap = 0; return RL_E_NOMEM; }
@@ -782,8 +765,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     mark(e, 7);
     // hot chains first (side stream), then the regions
-    HIP_OK(launch_region(ra, wide, res_bytes, s, e->split_hot ? e->hstream : nullptr, e->hot_ev[0],
-                         e->hot_ev[1], e->split_hot ? e->hstream2 : nullptr, e->hot_ev[2]));
+    HIP_OK(launch_region(ra, wide, res_bytes, s, e->hstream, e->hot_ev[0], e->hot_ev[1]));
     mark(e, 10);
     if (hot) HIP_OK(launch_hot_fill(ra, wide, res_bytes, s));
     // the next batch's routed regions: this batch's largest hot regions (two-pass tables)
@@ -1073,17 +1055,8 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
         e->sparse_max = (uint32_t)value;
         return RL_OK;
     }
-    if (std::strcmp(key, "region_walk") == 0) {       // 0 = one workgroup per region
-        if (value < 0 || value > 32) return RL_E_INVALID_ARG;
-        e->region_walk = (uint32_t)value;
-        return RL_OK;
-    }
     if (std::strcmp(key, "region_order") == 0) {
         e->region_order = value != 0;
-        return RL_OK;
-    }
-    if (std::strcmp(key, "chain3") == 0) {
-        e->chain3 = value != 0;
         return RL_OK;
     }
     if (std::strcmp(key, "order_prefix") == 0) {
@@ -1095,18 +1068,9 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
         e->route = value != 0;
         return RL_OK;
     }
-    if (std::strcmp(key, "split_hot") == 0) {
-        e->split_hot = value != 0;
-        return RL_OK;
-    }
     if (std::strcmp(key, "fail_batches") == 0) {      // the next `value` batches fail (RL_E_DEVICE)
         if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
         e->inject_fail = (uint32_t)value;
-        return RL_OK;
-    }
-    if (std::strcmp(key, "bin_shift") == 0) {
-        if (value != 0 && value != kBinShift) return RL_E_INVALID_ARG;
-        e->bin_shift = (int)value;
         return RL_OK;
     }
     return RL_E_INVALID_ARG;

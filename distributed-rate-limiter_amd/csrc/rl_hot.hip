@@ -237,14 +237,8 @@ hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, con
                            : F<CodecC, uint32_t>(__VA_ARGS__))
 
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
-                         hipStream_t hs, hipEvent_t e0, hipEvent_t e1, hipStream_t hs2, hipEvent_t e2) {
-    return RL_BY_WIDTH(region_launch_t, a, s, hs, e0, e1, hs2, e2);
-}
-hipError_t launch_hot_chains(const RegionArgs& a, bool wide, int res_bytes, hipStream_t hs, hipStream_t hs2) {
-    return RL_BY_WIDTH(hot_chains_t, a, hs, hs2);
-}
-hipError_t launch_regions_combined(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
-    return RL_BY_WIDTH(regions_combined_t, a, s);
+                         hipStream_t hs, hipEvent_t e0, hipEvent_t e1) {
+    return RL_BY_WIDTH(region_launch_t, a, s, hs, e0, e1);
 }
 hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
     return RL_BY_WIDTH(hot_fill_t, a, s);

@@ -337,37 +337,28 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
     }
 }
 
-// Phase B (one 3-wave workgroup per listed region, beside k_regions). Wave 0 (pass 1)
-// walks the region's summaries in arrival order with the hot key's threshold pair: a
-// group of 64 chunks, or a chunk, whose hot-key times all lie in [T0, T1) has its hot
-// records decided without being read (verdict + the key's state go back into the summary
-// for k_hot_fill); any other chunk has its hot records processed one by one (fast check,
-// then the wavefront-per-key sequential run). Wave 1 (pass 2), at the same time, applies
-// every other key of the region in arrival order, 64 records at a time through
-// wave_apply. The passes touch disjoint slots of the shared LDS table (wave 0 only the
-// hot key's state, wave 1 never that slot), so they need no synchronisation. Wave 2 runs
-// pass 1 for a second dominant key when the region holds one (HotInfo::ok bit 1); wave 1
-// then applies the records of neither key. WAVES = 1 (split launch, regions without a second
-// key): one wave runs pass 1 and then pass 2. A single-wave workgroup takes the first wave
-// slot that frees beside the normal regions; a 3-wave one waited for three on one CU, and
-// the later chains of sw_zipf started ~4 ms into the stage.
-template <class Codec, class Res, bool TOK, int WAVES = 3>
+// Phase B (one single-wave workgroup per listed region, beside k_regions). Pass 1 walks the
+// region's summaries in arrival order with the hot key's threshold pair: a group of 64
+// chunks, or a chunk, whose hot-key times all lie in [T0, T1) has its hot records decided
+// without being read (verdict + the key's state go back into the summary for k_hot_fill);
+// the other chunks are processed one by one (fast check, then the sequential run of the
+// key's state changes). Pass 1 runs again for a second dominant key when the region
+// holds one (HotInfo::ok bit 1). Pass 2 then applies every other key of the region in
+// arrival order, 64 records at a time through wave_apply. (A workgroup of one wave per pass
+// waited for its wave slots on one CU beside the normal regions: sw_zipf's later chains
+// started ~4 ms into the stage.)
+template <class Codec, class Res, bool TOK>
 __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Codec, true>& S) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
     __shared__ int32_t s_hslot[2];
     const uint32_t hc = min(a.hot_count[0], kHotMax);
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
     if (i >= hc) return;
     // the passes are sequential critical paths beside thousands of normal-region waves
     __builtin_amdgcn_s_setprio(3);
     const HotInfo f = a.hot_info[i];
-    if constexpr (WAVES == 1) {
-        if (a.chain_split == 2 && (f.ok & 2u)) return;   // two keys: the 3-wave launch's
-    } else {
-        if (a.chain_split && !(f.ok & 2u)) return;       // one key: the 1-wave launch's
-    }
-    const uint32_t region = f.bin;                    // bin_shift 0: bin == region
+    const uint32_t region = f.bin;                    // a bin is one region
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
     const int64_t lo = batch_lo(a.ctl);
@@ -384,7 +375,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     }
     const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     RL_GLOBAL Slot* tab = as_global((Slot*)L.table + (size_t)(region - L.region_base) * NS);
-    if (wid == 0) {
+    {
         // ---- load + rebuild the region (as k_regions), find or insert the hot key's slot
         Slot img[NS / 64];
 #pragma unroll
@@ -423,7 +414,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         }
         if (lane == 0) { s_hslot[0] = hsl[0]; s_hslot[1] = hsl[1]; }
     }
-    __syncthreads();
+    wave_fence();
     // hot_ok false (no dominant key, or its region is full): pass 2 takes every record; the
     // second key has a chain only beside the first's
     const int32_t hsl0 = s_hslot[0];
@@ -445,7 +436,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0, n_other = 0;
     uint32_t n_changed = 0, n_tk = 0, n_fb = 0;       // debug: changes, [T0, T1) updates,
     uint32_t n_late = 0;                              // detailed chunks starting before T0 / ending past T1
+    uint32_t n_prehit = 0;                            // debug: windows whose records were prefetched
     uint64_t cyc_run = 0, cyc_search = 0, cyc_detail = 0, cyc_pass2 = 0;   // debug stamps
+    uint64_t cyc_pre = 0, cyc_pass1 = 0;
     bool any_hot = false;
     auto pass1 = [&](auto algo, const uint32_t kk) {
         constexpr int A = decltype(algo)::value;
@@ -467,20 +460,87 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             if (!pred(g - 1)) return g;
             return wave_first_true(t0, g - 1, lane, pred);
         };
+        const uint64_t c_p1 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
         int64_t T0 = hot_t0<A>(lo, hi, sa, sb, sc);
         int64_t T1 = t1_of(T0);
-        // the hot records of one chunk (lane = arrival order inside the chunk). The next
-        // chunk's records are prefetched: undecided chunks come in runs.
+        // Sliding window: the allow-time table of the key's current window W. P(t) (the
+        // previous bucket, with its TTL lapse) is the same for every state the key passes
+        // through inside W (allows only INCR the current bucket, :114-116), so the first
+        // times at which an acquire of 1 or 2 permits is allowed with C = thr_c + lane in the
+        // current bucket, thr1 / thr2 (per lane; W + w = not in this window), hold until W
+        // ends: the allows of W are then found by integer compares, and [T0, T1) after a
+        // change is a table read instead of one lone wave's fp64 chain (the reference's
+        // arithmetic is only evaluated where the table is built, each entry verified there
+        // by the exact predicate, :158-180).
+        int64_t thr_w = INT64_MIN, thr_c = 0;           // table for window thr_w, counts thr_c + lane
+        int64_t thr1 = 0, thr2 = 0;
+        auto thr_build = [&](int64_t W, int64_t C) {     // (W, C wave-uniform; state sa, sb, sc)
+            const int64_t w = L.window_ms;
+            // the state after C - (its count in W) allows inside W: every lane's own count
+            SW2 s1 = sw_unpack(sa, sb, sc);
+            const int64_t cnt = C + (int64_t)lane;
+            if (s1.b1_start != W) {                      // roll into W (as sw_commit_allows)
+                if (s1.b1_start == W - w) { s1.b0_cnt = s1.b1_cnt; s1.b0_off = s1.b1_off; }
+                else { s1.b0_cnt = 0; s1.b0_off = 0; }
+                s1.b1_start = W;
+                s1.b1_off = 0;                           // (alive through W whatever it is)
+            }
+            s1.b1_cnt = (uint32_t)cnt;
+            const uint64_t la = (uint64_t)s1.b1_start;
+            const uint64_t lb = (uint64_t)s1.b1_cnt | ((uint64_t)s1.b0_cnt << 32);
+            const uint64_t lc = (uint64_t)(uint32_t)s1.b1_off | ((uint64_t)(uint32_t)s1.b0_off << 32);
+            const int64_t end = W + w;
+            auto first = [&](int64_t q) {                // first t in [W, W + w) allowing q
+                auto pred = [&](int64_t t) { return hot_pred_k<kAlgoSW>(L, t, la, lb, lc, q); };
+                int64_t g = hot_tk_guess<kAlgoSW>(L, W, la, lb, lc, q);
+                g = g < W ? W : g > end ? end : g;
+                // the guess is exact but at rounding edges: verify, step, else bisect
+                for (int it = 0; it < 2; ++it) {
+                    if (g > W && pred(g - 1)) --g;
+                    else if (g < end && !pred(g)) ++g;
+                    else return g;
+                }
+                if ((g == W || !pred(g - 1)) && (g == end || pred(g))) return g;
+                int64_t l = W, h = end;                  // pred false below l... true at h
+                while (l < h) {
+                    const int64_t m = l + (h - l) / 2;
+                    if (pred(m)) h = m; else l = m + 1;
+                }
+                return l;
+            };
+            thr1 = cnt + 1 <= L.max_permits ? first(1) : end;
+            thr2 = cnt + 2 <= L.max_permits ? first(2) : end;
+            thr_w = W;
+            thr_c = C;
+        };
+        // [T0, T1) for the current state from the table, when it covers it
+        auto t1_table = [&](int64_t t0, int64_t& t1) {
+            if constexpr (A != kAlgoSW) return false;
+            const SW2 s0 = sw_unpack(sa, sb, sc);
+            const int64_t W = s0.b1_start, w = L.window_ms;
+            if (W != thr_w || t0 < W || t0 >= W + w) return false;
+            const int64_t k = (int64_t)s0.b1_cnt - thr_c;
+            if (k < 0 || k > 63) return false;
+            const int64_t T = (int64_t)readlane64((uint64_t)thr1, (uint32_t)k);
+            t1 = T > hi + 1 ? hi + 1 : T;
+            if (t1 < t0) t1 = t0;
+            return true;
+        };
+        // The hot records of one chunk (lane = arrival order inside the chunk). The next chunk
+        // the walk details is prefetched (found from the group summaries once [T0, T1) is
+        // known), so its records are in flight while this chunk's results are stored.
         Rec pre = recs[min(f.start + lane, f.end - 1)];
         uint32_t pre_c = 0;
-        auto detail = [&](uint32_t c) {
+        // mn_l / mx_l / ns_l: this lane's chunk summary in the walked group; todo_after: the
+        // group's chunks still to walk after this one
+        auto detail = [&](uint32_t c, int64_t mn_l, int64_t mx_l, uint32_t ns_l, uint64_t todo_after) {
             ++n_detail;
             const uint64_t c_det = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
             const uint32_t j = f.start + c * kHotChunk + lane;
             const bool valid = j < f.end;
-            const Rec r = pre_c == c ? pre : recs[valid ? j : f.start];
-            pre_c = c + 1;
-            pre = recs[min(f.start + pre_c * kHotChunk + lane, f.end - 1)];
+            const bool use_pre = pre_c == c;
+            n_prehit += use_pre ? 1u : 0u;
+            const Rec r = use_pre ? pre : recs[valid ? j : f.start];
             const Req q = Codec::dec(r, base);
             const bool hot = is_key(q, valid);
             bool oa = false;
@@ -491,19 +551,22 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 orem = kRemUnknown;                       // :110-116, no state access
                 pend = false;
             }
-            {
+            // the pending prefix inside [T0, T1): denied, remaining 0
+            auto fast_prefix = [&]() {
                 const bool fast = q.op == (uint32_t)kOpAcquire && q.now_ms >= T0 && q.now_ms < T1;
                 const uint64_t m = __ballot(pend && !fast);
                 const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
-                if (pend && lane < first) {               // inside [T0, T1): denied, remaining 0
+                if (pend && lane < first) {
                     orem = 0;
                     if (TOK && A == kAlgoTB) tk = tb_refill(L, q.now_ms, sa, sb, sc);
                     pend = false;
                 }
-            }
+            };
+            fast_prefix();
             bool changed = false;
             bool t_fresh = false;                         // [T0, T1) is for the current state
             const uint64_t c_run = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+            if (a.dbg) cyc_pre += c_run - c_det;
             if constexpr (A == kAlgoTB) {
                 // token bucket: rounds; each applies the prefix up to the first state change
                 // (every earlier pending request is denied and leaves the state alone, Lua
@@ -535,76 +598,126 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                             T1 = t1_of(T0);
                             t_fresh = true;
                             ++n_tk;
-                            const bool fast = q.op == (uint32_t)kOpAcquire && q.now_ms >= T0 && q.now_ms < T1;
-                            const uint64_t m = __ballot(pend && !fast);
-                            const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;
-                            if (pend && lane < first) {
-                                oa = false;
-                                orem = 0;
-                                if (TOK) tk = tb_refill(L, q.now_ms, sa, sb, sc);
-                                pend = false;
-                            }
+                            fast_prefix();
                         }
                     }
                 }
             } else {
                 // sliding window: inside one window W the acquires only INCR the current
-                // bucket (:114-116), so with k allows before it a request's estimate is
-                // d2l(tv + (C0 + k)), tv = prev * pw at its own time (:174): the request is
-                // allowed iff k <= K, its largest such k. One pass computes tv and K per
-                // lane; the allows then follow by a greedy scan of integer compares (the
-                // k-th allow is the first request after the (k-1)-th with K >= k). Requests
-                // the scan cannot take (another window, before the newest bucket, a peek or
-                // a reset) run the exact step alone.
-                const SWGeo geo = pend ? sw_geo(q.now_ms, L) : SWGeo{};
+                // bucket (:114-116), so with k allows before it an acquire of p permits at t
+                // is allowed iff t >= T_p(C0 + k) (C0: the bucket's count before the chunk;
+                // the estimate is non-increasing in t inside W). The allows follow by a greedy
+                // scan: the k-th is the first request after the (k-1)-th at or past its
+                // threshold. Thresholds come from the window's table (p <= 2) or, per request,
+                // from the largest allowed k (K) by the closed form corrected by the exact
+                // predicate. Requests the scan cannot take (another window, before the newest
+                // bucket, near the epoch, a peek or a reset) run the exact step alone.
                 const int64_t w = L.window_ms, mx = L.max_permits;
                 while (__any(pend)) {
                     const uint32_t f0 = (uint32_t)__builtin_ctzll(__ballot(pend));
-                    const int64_t W0 = (int64_t)readlane64((uint64_t)geo.curr_start, f0);
-                    const bool scan = pend && q.op == (uint32_t)kOpAcquire && geo.curr_start == W0 &&
-                                      (int64_t)sa <= W0 && geo.prev_start != geo.curr_start;
+                    const int64_t t_f = (int64_t)readlane64((uint64_t)q.now_ms, f0);
+                    int64_t rr;
+                    const int64_t W0 = jdiv(t_f, w, L.inv_window, &rr) * w;     // t_f's window
+                    // (window membership by compares: no per-request division)
+                    const bool in_w = q.now_ms >= W0 && q.now_ms - W0 < w;
+                    const bool scan = pend && q.op == (uint32_t)kOpAcquire && in_w &&
+                                      (int64_t)sa <= W0 && t_f >= w;
                     const uint64_t und = __ballot(pend && !scan);
                     const uint32_t stop = und ? (uint32_t)__builtin_ctzll(und) : 64u;
                     const bool in = scan && lane < stop;
                     if (__any(in)) {
                         const SW2 s0 = sw_unpack(sa, sb, sc);
                         const int64_t C0 = s0.b1_start == W0 ? (int64_t)s0.b1_cnt : 0;
-                        const int64_t P = in ? sw_get(s0, geo.prev_start, q.now_ms, w) : 0;
-                        const double tv = (double)P * geo.prev_weight;           // :174, rounded
-                        auto est = [&](int64_t k) { return d2l(tv + (double)(C0 + k)); };
-                        int64_t K = mx - (int64_t)q.permits - C0 - (int64_t)tv;  // ~ largest k
-                        if (K >= 0 && est(K) + q.permits > mx) --K;             // rounding edges
-                        if (K >= 0 && est(K) + q.permits > mx) --K;
-                        if (est(K + 1) + q.permits <= mx) ++K;
-                        if (K < -1) K = -1;
-                        // greedy scan: kk = allows before this request inside the chunk
-                        int64_t kk = 0, k = 0;
+                        const bool small = !__any(in && q.permits > 2);
+                        if (small && (thr_w != W0 || C0 < thr_c || C0 - thr_c > 63)) {
+                            thr_build(W0, C0);
+                            ++n_tk;
+                        }
+                        int64_t kk = 0, na = 0;
                         bool al = false;
                         uint32_t cur = 0, last = 0;
-                        for (;;) {
-                            const uint64_t m = __ballot(in && lane >= cur && K >= k);
-                            if (in && lane >= cur) kk = k;
-                            if (!m) break;
-                            const uint32_t fa = (uint32_t)__builtin_ctzll(m);
-                            if (lane == fa) al = true;
-                            last = fa;
-                            ++k;
-                            cur = fa + 1;
+                        if (small) {
+                            // greedy scan on the table: the na-th allow is the first request
+                            // at or past T_p(C0 + na); rebuilt when the window fills it
+                            for (;;) {
+                                if (C0 + na - thr_c > 63) {     // (wave-uniform) table exhausted
+                                    thr_build(W0, C0 + na);
+                                    ++n_tk;
+                                }
+                                const uint32_t ix = (uint32_t)(C0 + na - thr_c);
+                                const int64_t u1 = (int64_t)readlane64((uint64_t)thr1, ix);
+                                const int64_t u2 = (int64_t)readlane64((uint64_t)thr2, ix);
+                                const bool cnd = in && lane >= cur;
+                                const uint64_t m = __ballot(cnd && q.now_ms >= (q.permits == 1 ? u1 : u2));
+                                if (cnd) kk = na;
+                                if (!m) break;
+                                const uint32_t fa = (uint32_t)__builtin_ctzll(m);
+                                if (lane == fa) al = true;
+                                last = fa;
+                                ++na;
+                                cur = fa + 1;
+                            }
+                            // remaining after the request: max - est(C0 + kk (+1)) = the number
+                            // of q <= 2 with T_q at or before t; 2 or more: the exact estimate
+                            const int64_t cc = C0 + kk + (al ? 1 : 0);
+                            const int64_t ixl = cc - thr_c;
+                            const bool tab = ixl >= 0 && ixl <= 63;
+                            const int src = (int)(tab ? ixl : 0);
+                            const int64_t v1 = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)thr1 >> 32), src, 64) << 32) |
+                                                         (uint32_t)__shfl((int)(uint32_t)thr1, src, 64));
+                            const int64_t v2 = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)thr2 >> 32), src, 64) << 32) |
+                                                         (uint32_t)__shfl((int)(uint32_t)thr2, src, 64));
+                            if (in) {
+                                int64_t rem;
+                                if (tab && q.now_ms < v1) rem = 0;
+                                else if (tab && q.now_ms < v2) rem = 1;
+                                else {
+                                    const SWGeo g = sw_geo(q.now_ms, L);
+                                    const double t = (double)sw_get(s0, g.prev_start, q.now_ms, w) * g.prev_weight;
+                                    const int64_t e = d2l(t + (double)cc);
+                                    rem = mx - e > 0 ? mx - e : 0;
+                                }
+                                oa = al;
+                                orem = rem;
+                                n_allowed += al ? 1u : 0u;
+                                pend = false;
+                            }
+                        } else {
+                            const SWGeo g = in ? sw_geo(q.now_ms, L) : SWGeo{};
+                            const int64_t P = in ? sw_get(s0, g.prev_start, q.now_ms, w) : 0;
+                            const double tv = (double)P * g.prev_weight;             // :174, rounded
+                            auto est = [&](int64_t k) { return d2l(tv + (double)(C0 + k)); };
+                            int64_t K = -1;
+                            if (in) {
+                                K = mx - (int64_t)q.permits - C0 - (int64_t)tv;      // ~ largest k
+                                if (K >= 0 && est(K) + q.permits > mx) --K;         // rounding edges
+                                if (K >= 0 && est(K) + q.permits > mx) --K;
+                                if (est(K + 1) + q.permits <= mx) ++K;
+                                if (K < -1) K = -1;
+                            }
+                            for (;;) {
+                                const uint64_t m = __ballot(in && lane >= cur && K >= na);
+                                if (in && lane >= cur) kk = na;
+                                if (!m) break;
+                                const uint32_t fa = (uint32_t)__builtin_ctzll(m);
+                                if (lane == fa) al = true;
+                                last = fa;
+                                ++na;
+                                cur = fa + 1;
+                            }
+                            if (in) {
+                                const int64_t e = est(al ? kk + 1 : kk);             // after the request
+                                oa = al;
+                                orem = mx - e > 0 ? mx - e : 0;
+                                n_allowed += al ? 1u : 0u;
+                                pend = false;
+                            }
                         }
-                        if (in) {
-                            const int64_t e = est(al ? kk + 1 : kk);             // after the request
-                            oa = al;
-                            orem = mx - e > 0 ? mx - e : 0;
-                            n_allowed += al ? 1u : 0u;
-                            pend = false;
-                        }
-                        if (k > 0) {
-                            const int64_t t_last = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(
-                                (int)(uint32_t)(q.now_ms >> 32), (int)last) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)q.now_ms, (int)last));
+                        if (na > 0) {
+                            const int64_t t_last = (int64_t)readlane64((uint64_t)q.now_ms, last);
                             SWGeo gl{};
                             gl.curr_start = W0;
-                            sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)k, t_last);
+                            sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)na, t_last);
                             changed = true;
                         }
                     }
@@ -623,6 +736,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         if (o.mutate) {
                             sa = o.a; sb = o.b; sc = o.c;
                             changed = true;
+                            thr_w = INT64_MIN;               // P may have changed: rebuild
                         }
                     }
                 }
@@ -640,7 +754,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 // computed after the last change
             } else if (changed) {
                 T0 = hot_t0<A>(lo, hi, sa, sb, sc);
-                T1 = t1_of(T0);
+                if (!t1_table(T0, T1)) T1 = t1_of(T0);
                 ++n_tk;
             } else if (T1 < hi && __any(hot && q.op == (uint32_t)kOpAcquire && q.now_ms >= T1)) {
                 // no change although requests lay past T1: T1 was only a lower bound of the
@@ -650,12 +764,20 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                                      [&](int64_t t) { return hot_pred_k<A>(L, t, sa, sb, sc, 1); });
                 ++n_tk;
             }
+            // the next chunk the walk will detail: the first one left in the group that the
+            // new [T0, T1) does not decide (else the next chunk); its loads go out now
+            {
+                const bool skip_l = ns_l == 0 && mn_l >= T0 && mx_l < T1;
+                const uint64_t nx = todo_after & ~__ballot(skip_l);
+                pre_c = nx ? (c & ~63u) + (uint32_t)__builtin_ctzll(nx) : c + 1;
+                pre = recs[min(f.start + pre_c * kHotChunk + lane, f.end - 1)];
+            }
             if (a.dbg) {
                 const uint64_t c_end = __builtin_amdgcn_s_memtime();
                 cyc_run += c_srch - c_run;
                 cyc_search += c_end - c_srch;
             }
-            if (hot) {
+            if (hot && !(a.ablate & kAblNoChainStores)) {
                 put_res<Res>(a, j, oa, orem);
                 if (TOK) a.tok[j] = tk;
             }
@@ -696,7 +818,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                     n_fb += fmn < T0 ? 1u : 0u;
                     n_late += fmx >= T1 ? 1u : 0u;
                 }
-                detail(grp * 64 + fst);
+                detail(grp * 64 + fst, mn, mx, ns, todo);
             }
         };
         // level 2: 64 groups per test, the next 64 in flight
@@ -729,6 +851,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 walk_group(g0 + fst);
             }
         }
+        if (a.dbg) cyc_pass1 += __builtin_amdgcn_s_memtime() - c_p1;
     };
     auto pass2 = [&](auto algo) {
         constexpr int A = decltype(algo)::value;
@@ -741,7 +864,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             uint32_t n_hits = 0;                          // (no local cache on the hot path)
             const Applied ap = wave_apply<Codec, A, false>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
-            if (v) {
+            if (v && !(a.ablate & kAblNoChainStores)) {
                 put_res<Res>(a, ap.j, ap.alw, ap.rem);
                 if (TOK) a.tok[ap.j] = ap.tok;
             }
@@ -818,25 +941,14 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         if (count > 0) apply64(count);
         if (a.dbg) cyc_pass2 += __builtin_amdgcn_s_memtime() - c_p2;
     };
-    if constexpr (WAVES == 1) {
-        if (L.algo == kAlgoTB) {
-            if (hot_ok) pass1(std::integral_constant<int, kAlgoTB>{}, 0u);
-            if (hot_ok2) pass1(std::integral_constant<int, kAlgoTB>{}, 1u);
-            pass2(std::integral_constant<int, kAlgoTB>{});
-        } else {
-            if (hot_ok) pass1(std::integral_constant<int, kAlgoSW>{}, 0u);
-            if (hot_ok2) pass1(std::integral_constant<int, kAlgoSW>{}, 1u);
-            pass2(std::integral_constant<int, kAlgoSW>{});
-        }
-    } else if (wid == 0 || wid == 2) {
-        const uint32_t kk = wid >> 1;
-        if (kk ? hot_ok2 : hot_ok) {
-            if (L.algo == kAlgoTB) pass1(std::integral_constant<int, kAlgoTB>{}, kk);
-            else pass1(std::integral_constant<int, kAlgoSW>{}, kk);
-        }
+    if (L.algo == kAlgoTB) {
+        if (hot_ok) pass1(std::integral_constant<int, kAlgoTB>{}, 0u);
+        if (hot_ok2) pass1(std::integral_constant<int, kAlgoTB>{}, 1u);
+        pass2(std::integral_constant<int, kAlgoTB>{});
     } else {
-        if (L.algo == kAlgoTB) pass2(std::integral_constant<int, kAlgoTB>{});
-        else pass2(std::integral_constant<int, kAlgoSW>{});
+        if (hot_ok) pass1(std::integral_constant<int, kAlgoSW>{}, 0u);
+        if (hot_ok2) pass1(std::integral_constant<int, kAlgoSW>{}, 1u);
+        pass2(std::integral_constant<int, kAlgoSW>{});
     }
     for (int off = 32; off > 0; off >>= 1) {
         n_allowed += __shfl_xor(n_allowed, off, 64);
@@ -850,13 +962,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
     }
     // ---- write the region back, statistics
-    __shared__ uint64_t s_w1[2];                      // wave 1's debug counters
-    if (wid == (WAVES == 1 ? 0u : 1u) && lane == 0) { s_w1[0] = n_other; s_w1[1] = cyc_pass2; }
-    const bool touched0 = __syncthreads_or(wid == 0 && any_hot);
-    const bool touched1 = __syncthreads_or((WAVES == 1 ? wid == 0 : wid == 2) && any_hot);
-    if (wid != 0) return;
-    if (lane == 0 && hot_ok && touched0) S.occ[hsl0] |= 2u;
-    if (lane == 0 && hot_ok2 && touched1) S.occ[hsl1] |= 2u;
+    const bool hot_touched = __any(any_hot);
+    if (lane == 0 && hot_ok && hot_touched) S.occ[hsl0] |= 2u;
+    if (lane == 0 && hot_ok2 && hot_touched) S.occ[hsl1] |= 2u;
     wave_fence();
     uint32_t touched = 0, used = 0;
     for (uint32_t sl = lane; sl < NS; sl += 64) {
@@ -884,34 +992,25 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             d[3] = (uint64_t)n_detail | (uint64_t)min(n_tk, 0xFFFFu) << 32 | (uint64_t)min(n_fb, 0x7FFFu) << 48 | (1ULL << 63);
             d[4] = cyc_detail; d[5] = cyc_run; d[6] = cyc_search;
             d[7] = min((uint64_t)n_changed, (uint64_t)0xFFFFFF) | min((uint64_t)n_late, (uint64_t)0xFFFFFF) << 24;
+            d[8] = cyc_pre; d[9] = cyc_pass1; d[10] = cyc_pass2; d[11] = n_other; d[12] = n_prehit;
         }
     }
 }
 
-// One launch for both (rl_tune split_hot = 0): 3-wave workgroups; the first kHotMax run the
-// hot regions' chains, the rest three normal regions each, so the chains are dispatched
-// before the normal regions fill the machine, at the LDS per wave of the plain kernel.
+// The hot chains alone (single-wave workgroups), launched on a side stream of the device's
+// highest priority just before the normal regions' launch, so they start first. They are a
+// few hundred lone waves beside ~10^6 normal-region waves: a larger register budget costs
+// no occupancy that matters.
+#ifndef RL_CHAIN_MIN_WAVES
+#define RL_CHAIN_MIN_WAVES 2
+#endif
 template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(192, RL_HOT_MIN_WAVES) void k_regions_hot(RegionArgs a) {
-    __shared__ union U { RegionTable three[3]; RegionLds<Codec, true> one; } S;
-    if (blockIdx.x < kHotMax) {
-        hot_chain<Codec, Res, TOK>(a, blockIdx.x, S.one);
-        return;
-    }
-    region_body_t<Codec, Res, TOK, 0>(a, (blockIdx.x - kHotMax) * 3 + (threadIdx.x >> 6),
-                                      S.three[threadIdx.x >> 6]);
-}
-
-// The hot chains alone (3-wave workgroups), launched on a side stream just before the
-// normal regions' single-wave launch: no normal region waits for another region of a
-// multi-wave workgroup, and the chains still start first.
-template <class Codec, class Res, bool TOK, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, RL_HOT_MIN_WAVES) void k_hot_chains(RegionArgs a) {
+__global__ __launch_bounds__(64, RL_CHAIN_MIN_WAVES) void k_hot_chains(RegionArgs a) {
     __shared__ RegionLds<Codec, true> S;
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     for (uint32_t i = blockIdx.x; i < hc; i += gridDim.x) {       // (workgroup-uniform)
-        if (i != blockIdx.x) __syncthreads();                     // the last chain's LDS users
-        hot_chain<Codec, Res, TOK, WAVES>(a, i, S);
+        wave_fence();                                             // the last chain's LDS users
+        hot_chain<Codec, Res, TOK>(a, i, S);
     }
 }
 
@@ -972,27 +1071,12 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
     }
 }
 
-// Split launch: single-key regions' chains as 1-wave workgroups on hs, two-key regions' as
-// 3-wave workgroups on hs2 (each launch skips the other's entries).
+// The chain launch: single-wave workgroups on the side stream hs.
 template <class Codec, class Res>
-hipError_t hot_chains_t(const RegionArgs& a_in, hipStream_t hs, hipStream_t hs2) {
-    RegionArgs a = a_in;
-    a.chain_split = a_in.chain3 ? 2u : 1u;      // chain3 0: single waves take every region
+hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs) {
     const dim3 g(a.chain_grid ? min(a.chain_grid, kHotMax) : kHotMax);
-    if (a.tok) {
-        hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 1>), g, dim3(64), 0, hs, a);
-        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, 3>), g, dim3(192), 0, hs2, a);
-    } else {
-        hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 1>), g, dim3(64), 0, hs, a);
-        if (a.chain3) hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, 3>), g, dim3(192), 0, hs2, a);
-    }
-    return hipGetLastError();
-}
-template <class Codec, class Res>
-hipError_t regions_combined_t(const RegionArgs& a, hipStream_t s) {
-    const dim3 g(kHotMax + (a.n_regions + 2) / 3), b2(192);
-    if (a.tok) hipLaunchKernelGGL((k_regions_hot<Codec, Res, true>), g, b2, 0, s, a);
-    else hipLaunchKernelGGL((k_regions_hot<Codec, Res, false>), g, b2, 0, s, a);
+    if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true>), g, dim3(64), 0, hs, a);
+    else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false>), g, dim3(64), 0, hs, a);
     return hipGetLastError();
 }
 template <class Codec, class Res>

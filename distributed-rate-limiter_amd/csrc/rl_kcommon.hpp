@@ -7,18 +7,19 @@
 // the other requests of its (limiter, key) WITHOUT a full sort:
 //
 //   1. k_upsweep  : per 64K-request tile, histogram of the partition digit of each
-//                   request's BIN (bin = 8 consecutive state-table regions; region =
-//                   top bits of mix64(key)).
+//                   request's BIN (one state-table region; region = top bits of
+//                   mix64(key) below the shard bits).
 //   2. k_scan_rows/k_scan_small : exclusive scan of the [bin][tile] histogram.
 //   3. k_scatter  : stable partition (wave ballot-match ranking) of the requests
 //                   into bin order, packed into 16-byte records.
 //   (1-3 repeat once more when a limiter set has > 1024 bins.)
 //   4. k_regions  : one single-wave workgroup per REGION. The wave loads its region's
-//                   256 state slots (8 KB) into LDS once, streams its bin's records
-//                   in arrival order, keeps its region's requests in an LDS ring and
-//                   applies the reference semantics per key in order, 64 at a time
-//                   (deny never mutates, so a group needs 1 + (#state changes of its
-//                   busiest key) rounds); the region is written back once.
+//                   256 state slots (8 KB) into LDS once (or faults in single buckets of
+//                   a sparse region), streams the region's records in arrival order and
+//                   applies the reference semantics per key in order, 64 at a time (SW:
+//                   a greedy scan per key; TB: 1 + (#state changes of its busiest key)
+//                   rounds, deny never mutates); the region is written back once. Hot
+//                   regions run as chains beside it (rl_hot.hpp).
 //   5. k_unpermute: results back to the caller's order (allowed u8, remaining i64).
 //
 // Partition and unpermute grids are persistent and walk tiles XCD-aware: at any
@@ -221,7 +222,7 @@ __device__ inline uint32_t bin_of(const PartArgs& a, uint32_t i, const LimLds& L
         h = r->h;
         lim = Codec::limiter_of(*r);
     }
-    return (L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift;
+    return L.base[lim] + region_local(h, a.shard_bits, L.bits[lim]);
 }
 
 // Routed regions (pass 0): the route table (kRouteSlots region ids) in LDS; a region is

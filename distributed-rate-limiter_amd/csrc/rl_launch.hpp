@@ -20,6 +20,7 @@ enum : uint32_t {
     kAblNoProbe = 1u << 9,       // region: slot = home (no lookup / insert)
     kAblNoRounds = 1u << 10,     // region: one round, no peer match
     kAblNoNormal = 1u << 11,     // region: skip every non-hot region (hot chains run alone)
+    kAblNoChainStores = 1u << 12,// hot chains: skip the result stores (measures their waits)
     kAblNoGather = 1u << 16,     // unpermute: skip the res gather
 };
 
@@ -69,7 +70,6 @@ struct PartArgs {
     const DevLimiter* lims;
     int32_t digit_shift;
     int32_t digit_bits;
-    int32_t bin_shift;         // bin = region >> bin_shift (0: one region per bin, 3: eight)
     uint32_t up_per_cu;        // persistent-grid workgroups per CU (0: default)
     uint32_t sc_per_cu;
     uint32_t sc_split;         // rl_tune("scatter_split"): loads and stores in separate waves
@@ -103,10 +103,9 @@ struct RegionArgs {
     int64_t* ext;              // remaining of results stored as kResEscape (same positions)
     double* tok;               // nullable: TB fp64 balances in region order
     BatchCtl* ctl;
-    uint32_t n_regions;        // multiple of kRegionsPerBin; one workgroup per bin
+    uint32_t n_regions;        // one workgroup per region (= partition bin)
     uint32_t n_total;          // batch size: res/tok carry 64 padding entries past it
     int32_t shard_bits;
-    int32_t bin_shift;
     uint32_t ablate;
     int64_t skew_ms;           // rl_opts.max_skew_ms: slots kept until dead at batch min - skew
     unsigned long long* stats; // [kStatSlots][8] sharded batch counters (k_stats_reduce)
@@ -114,7 +113,7 @@ struct RegionArgs {
     uint32_t sparse_max;       // one region per bin: a region with <= this many records
                                // probes single buckets in HBM instead of loading its image
     const uint32_t* rend;      // nullable: bin b holds records [rstart[b], rend[b]) (2 passes)
-    // hot regions (bin_shift 0): k_hot_select lists the largest bins (>= hot_threshold
+    // hot regions: k_hot_select lists the largest bins (>= hot_threshold
     // records, at most kHotMax); the k_hot_* kernels own them (hot_mark[bin] == epoch),
     // k_regions skips them.
     const uint32_t* hot_list;  // [kHotMax]
@@ -126,19 +125,13 @@ struct RegionArgs {
                                // (words 0-3 the dominant key, 4-7 the second key)
     uint64_t* hot_summ2;       // [groups][8]: the same over 64 chunks (4096 records)
     uint32_t* hot_total;       // [0] chunks, [1] groups over the listed regions
-    uint32_t* work;            // region walk (walk > 0): 8 claim counters, 64 B apart, zeroed
-    uint32_t walk;             // rl_tune("region_walk"): persistent normal-region waves per CU
-                               // claiming regions from `work` (0: one workgroup per region)
     uint64_t* dbg;             // nullable (rl_tune "debug_regions"): per bin kDbgWords words
                                // {t_start, t_end, records, rounds, 4 x cycle counters}
     // nullable: dispatch order of the normal regions, largest size class first (block g runs
     // region order[g]; order[n_regions] = number of non-empty regions listed)
     const uint32_t* order;
     uint32_t order_prefix;     // that many of the smallest regions are dispatched first
-    uint32_t chain_split;      // (set by the launcher) 1: single-wave chains take every region;
-                               // 2: two-key regions go to the 3-wave launch
-    uint32_t chain3;           // rl_tune("chain3"): two-key regions as 3-wave workgroups
-    uint32_t chain_grid;       // workgroups of the chain launches (each loops over the hot list
+    uint32_t chain_grid;       // workgroups of the chain launch (each loops over the hot list
                                // with that stride): sized on the host from an earlier batch's
                                // hot count, so a batch with no hot region launches few idle ones
     // routed hot regions (hot_list entries with kHotRoutedBit): region, first record, count
@@ -175,7 +168,7 @@ __host__ __device__ inline void route_slots(uint32_t region, uint32_t& s1, uint3
     s2 = ((region ^ 0x5BD1E995u) * 0x85EBCA6Bu) >> 21;
 }
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
-constexpr uint32_t kDbgWords = 8;        // debug words per bin
+constexpr uint32_t kDbgWords = 16;       // debug words per bin
 // Batch counters are sharded: one device-scope atomic word sustains only ~88 adds per us
 // (MI355X_MICROARCH.md, rows 'dequeue' / 'fanin'), and every region wave adds to them, so a
 // 1.3M-region batch on ONE set of words serialises for >10 ms. Region waves add to slot
@@ -203,7 +196,6 @@ struct BoundsArgs {
     uint32_t n_lim;
     const DevLimiter* lims;
     int32_t shard_bits;
-    int32_t bin_shift;
     uint32_t* rstart;          // [n_bins]
     uint32_t* rend;            // [n_bins]
     const uint32_t* hi_base;   // [2^d1] first record of each high-digit run (pass-1 scan)
@@ -291,20 +283,13 @@ hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, ui
 hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hipStream_t s);
 hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
                            uint32_t cols, hipStream_t s);
-// hs (nullable): side stream for the hot chains (k_hot_chains), ordered by events e0 / e1;
-// without it the chains share the normal regions' launch (2-wave workgroups).
+// hs (nullable): side stream for the hot chains (k_hot_chains), ordered by events e0 / e1.
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
-                         hipStream_t hs = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
-                         hipStream_t hs2 = nullptr, hipEvent_t e2 = nullptr);
-// the hot chains' side-stream launch, and the one-launch variant (split_hot 0)
-hipError_t launch_hot_chains(const RegionArgs& a, bool wide, int res_bytes, hipStream_t hs, hipStream_t hs2);
-hipError_t launch_regions_combined(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
+                         hipStream_t hs = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // per record codec / packed result width (instantiated in csrc/rl_rt_*.hip)
 template <class Codec, class Res>
-hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0, hipEvent_t e1,
-                           hipStream_t hs2, hipEvent_t e2);
-template <class Codec, class Res> hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs, hipStream_t hs2);
-template <class Codec, class Res> hipError_t regions_combined_t(const RegionArgs& a, hipStream_t s);
+hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0, hipEvent_t e1);
+template <class Codec, class Res> hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs);
 template <class Codec, class Res> hipError_t hot_fill_t(const RegionArgs& a, hipStream_t s);
 hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s);
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s);   // prep, scan, summaries

@@ -238,12 +238,12 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
                     }
                     // routing: the upsweep's digit (route-table lookup done once per request)
                     d = a.digit ? in.dig_v(a)
-                                : (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                                : ((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim]))
                                    >> a.digit_shift) & ((1u << a.digit_bits) - 1);
                 } else {
                     rec = in.rec;
                     const uint32_t lim = Codec::limiter_of(rec);
-                    d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                    d = ((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim]))
                          >> a.digit_shift) & ((1u << a.digit_bits) - 1);
                 }
             }
@@ -376,12 +376,12 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
                 mx = k > mx ? k : mx;
             }
             d = a.digit ? in.dig_v(a)
-                        : (((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+                        : ((L.base[lim] + region_local(h, a.shard_bits, L.bits[lim]))
                            >> a.digit_shift) & ((1u << a.digit_bits) - 1);
         } else {
             rec = in.rec;
             const uint32_t lim = Codec::limiter_of(rec);
-            d = (((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim])) >> a.bin_shift)
+            d = ((L.base[lim] + region_local(rec.h, a.shard_bits, L.bits[lim]))
                  >> a.digit_shift) & ((1u << a.digit_bits) - 1);
         }
     };
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(256) void k_bin_bounds(BoundsArgs a) {
     auto lo_of = [&](uint32_t i) {
         const typename Codec::Rec r = recs[i];
         const uint32_t lim = Codec::limiter_of(r);
-        return ((s_base[lim] + region_local(r.h, a.shard_bits, s_bits[lim])) >> a.bin_shift) & lo_mask;
+        return (s_base[lim] + region_local(r.h, a.shard_bits, s_bits[lim])) & lo_mask;
     };
     const uint32_t hi = blockIdx.x;
     const uint32_t beg = a.hi_base[hi], end = beg + a.hi_total[hi];

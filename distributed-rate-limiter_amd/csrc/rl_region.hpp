@@ -8,12 +8,10 @@
 namespace rl {
 
 // ------------------------------------------------------------------ 4. regions
-// One single-wave workgroup per REGION. The region's 256 slots (8 KB) live in the wave's
-// LDS for the whole batch. The wave streams its BIN's records (arrival order, 8
-// regions interleaved) 64 at a time, keeps the ones of its region in an LDS ring and
-// applies them 64 at a time. The 8 waves of a bin have block ids congruent mod 8 and
-// adjacent in dispatch order, i.e. they run together on one XCD, so the bin's stream is
-// fetched from HBM once and re-read from that XCD's L2. No barriers anywhere.
+// One single-wave workgroup per REGION (a partition bin is one region). The region's 256
+// slots (8 KB) live in the wave's LDS for the whole batch (or, for a sparse region, only the
+// 4-slot buckets its probes reach); the wave streams the region's records in arrival order,
+// kDepth slices of 64 in flight, and applies them 64 at a time. No barriers anywhere.
 
 
 struct RegionTable {
@@ -23,11 +21,6 @@ struct RegionTable {
     uint64_t sb[kRegionSlots];
     uint64_t sc[kRegionSlots];
     alignas(16) uint32_t occ[kRegionSlots];   // bit0 occupied, bit1 touched by this batch
-#ifdef RL_CHAINS
-    int64_t xrem[64];                         // wave_apply's per-key chains: results by lane
-    double xtok[64];
-    uint32_t xalw[64];
-#endif
 };
 // With a sliding-window local cache (SlidingWindowRateLimiter.java:57-64): every slot also
 // carries its key's cache state (block-until ms, sw_step_cache), moved with the slot.
@@ -39,7 +32,7 @@ struct RegionTableX : RegionTable {
 template <class Codec, bool RING>
 struct RegionLds : RegionTable {
     using Rec = typename Codec::Rec;
-    Rec ring[kRing];                  // this region's pending requests (bins of 8 regions)
+    Rec ring[kRing];                  // pending requests of the other keys (hot chains)
     uint32_t ring_pos[kRing];         // ... and their result index
 };
 template <class Codec>
@@ -110,58 +103,6 @@ __device__ inline void note_fill(const RegionArgs& a, uint32_t region, uint32_t 
         atomicOr(&a.ctl->grow[li >> 6], 1ULL << (li & 63));
     }
 }
-
-#ifdef RL_CHAINS
-// A/B build only (-DRL_CHAINS): measured slower than the rounds on every bench config
-// (same-box A/B: tb_uniform region 1.21 -> 1.28 ms, zipf_1b 6.16 -> 6.64, mixed 13.93 -> 14.03).
-// The per-key chains of wave_apply: every pending lane's key has its state in S[slot]; the
-// lowest pending lane of each key runs that key's pending requests in lane (= arrival) order,
-// reading each request's fields from its lane; results go through LDS back to their lanes.
-template <class Codec, int ALGO, class LdsT>
-__device__ inline void wave_chains(LdsT& S, const DevLimiter& L, uint32_t lane, const Req& q,
-                                   const SWGeo& geo, int32_t slot, bool& pending, uint64_t kp,
-                                   Applied& r, uint32_t& n_allowed) {
-    const bool leader = pending && (kp & ((1ULL << lane) - 1)) == 0;
-    uint64_t todo = leader ? kp : 0ULL;
-    uint64_t sa = 0, sb = 0, sc = 0;
-    if (leader) { sa = S.sa[slot]; sb = S.sb[slot]; sc = S.sc[slot]; }
-    while (__any(todo != 0)) {
-        const bool act = todo != 0;
-        const uint32_t l = act ? (uint32_t)__builtin_ctzll(todo) : lane;
-        todo &= todo - 1;
-        // every lane takes part in the shuffles (a source lane may be idle)
-        const int64_t t_l = __shfl(q.now_ms, (int)l, 64);
-        const int32_t p_l = __shfl(q.permits, (int)l, 64);
-        const uint32_t op_l = (uint32_t)__shfl((int)q.op, (int)l, 64);
-        Outcome o{};
-        if constexpr (ALGO == kAlgoTB) {
-            if (act) o = tb_step(L, op_l, p_l, t_l, sa, sb, sc);
-        } else {
-            SWGeo g;
-            g.curr_start = __shfl(geo.curr_start, (int)l, 64);
-            g.prev_start = __shfl(geo.prev_start, (int)l, 64);
-            g.prev_weight = __shfl(geo.prev_weight, (int)l, 64);
-            if (act) o = sw_step_g(L, op_l, p_l, t_l, g, sa, sb, sc);
-        }
-        if (act) {
-            S.xrem[l] = o.remaining;
-            S.xtok[l] = o.tokens;
-            S.xalw[l] = o.allowed ? 1u : 0u;
-            if (o.mutate) { sa = o.a; sb = o.b; sc = o.c; }
-        }
-    }
-    if (leader) { S.sa[slot] = sa; S.sb[slot] = sb; S.sc[slot] = sc; }
-    wave_fence();
-    if (pending) {
-        r.alw = S.xalw[lane] != 0;
-        r.rem = S.xrem[lane];
-        r.tok = S.xtok[lane];
-        n_allowed += r.alw ? 1u : 0u;
-        pending = false;
-    }
-    wave_fence();
-}
-#endif
 
 // Apply one group of up to 64 requests (lane order = arrival order; `valid` lanes only).
 // SP: the region may be sparse (unloaded buckets, tombstones); image regions (SP = false)
@@ -371,26 +312,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         }
         return r;
     } else {
-    [[maybe_unused]] uint32_t my_rounds = 0;      // -DRL_CHAINS only
     while (__any(pending)) {
-        // Chains: after two rounds, if every key still pending has changed state in (nearly)
-        // every round so far (runs of TB allows, SW allows across windows) and some key still
-        // has >= 4 requests pending, the rounds would go on finalizing one request per key
-        // each; the lowest pending lane of every key then applies the key's remaining
-        // requests itself, in arrival order (each a full exact step; a deny leaves the state
-        // as it is), instead of one wave round per state change.
-#ifdef RL_CHAINS
-        if (!CACHE && my_rounds >= 2 && !one_round) {
-            const uint64_t kp = peers & __ballot(pending);
-            const uint32_t fin = (uint32_t)__popcll(peers) - (uint32_t)__popcll(kp);
-            if (__all(!pending || fin <= 2u * my_rounds) && __any(pending && __popcll(kp) >= 4)) {
-                ++n_rounds;
-                wave_chains<Codec, ALGO>(S, L, lane, q, geo, slot, pending, kp, r, n_allowed);
-                break;
-            }
-        }
-#endif
-        ++my_rounds;
         ++n_rounds;
         Outcome o{};
         SWAllow al{false, 0};
@@ -497,15 +419,13 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
     }
 }
 
-template <class Codec, class Res, bool TOK, int BS, class LdsT>
+template <class Codec, class Res, bool TOK, class LdsT>
 __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
-    constexpr uint32_t RPB = 1u << BS;              // regions per bin
 
-    // RPB = 8: block g = 64q + 8r + x  ->  bin 8q + x, region r of that bin (see above)
-    uint32_t bin = RPB == 1 ? g : (g / 64) * 8 + (g % 8);
-    if (RPB == 1 && a.order) {
+    uint32_t bin = g;
+    if (a.order) {
         // largest regions first (k_order_place), after a prefix of the smallest: the first
         // workgroups the machine takes then finish quickly and the hot chains (a side
         // stream of higher priority) get their slots at once instead of behind the longest
@@ -515,8 +435,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         const uint32_t k = min(a.order_prefix, tot);
         bin = a.order[g < k ? tot - k + g : g - k];
     }
-    const uint32_t rb = RPB == 1 ? 0u : (g / 8) % 8;
-    const uint32_t n_bins = a.n_regions / RPB;
+    const uint32_t n_bins = a.n_regions;
     if (bin >= n_bins) return;
     if (a.hot_mark && a.hot_mark[bin] == a.epoch) return;     // owned by hot_chain
     if (a.ablate & kAblNoNormal) return;
@@ -525,7 +444,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     if (cnt == 0) return;
     const uint32_t end = start + cnt;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t region = bin * RPB + rb;
+    const uint32_t region = bin;
     const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = a.ctl->base_ms;
     const int64_t batch_min = keep_from(a);
@@ -535,21 +454,17 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
 
     if (a.ctl->span_overflow != 0) {
         // compact records cannot represent this batch's time span: reject it whole,
-        // before any state is touched (the host reports RL_E_INVALID_ARG). Wave rb of
-        // the bin writes its region's share.
+        // before any state is touched (the host reports RL_E_INVALID_ARG)
         for (uint32_t j = start + lane; j < end; j += 64) {
-            const Rec r = recs[j];
-            if ((region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb) {
-                res[j] = (Res)pack_result(false, kRemInvalid);
-                if (TOK) a.tok[j] = __builtin_nan("");
-            }
+            res[j] = (Res)pack_result(false, kRemInvalid);
+            if (TOK) a.tok[j] = __builtin_nan("");
         }
         return;
     }
-    // kDepth slices of the bin's stream in flight (issued while the region image loads)
+    // kDepth slices of the region's stream in flight (issued while the region image loads);
+    // the stream is read once (non-temporal)
     constexpr uint32_t kDepth = 4;
-    // unconditional; read once when the bin is the region (streaming), else shared by RPB waves
-    auto fetch = [&](uint32_t c) { return ld_rec<kNtRgRec && RPB == 1>(recs + min(c + lane, end - 1)); };
+    auto fetch = [&](uint32_t c) { return ld_rec<kNtRgRec>(recs + min(c + lane, end - 1)); };
     Rec q0 = fetch(start), q1 = fetch(start + 64), q2 = fetch(start + 128), q3 = fetch(start + 192);
 
     // ---- load the region, dropping entries no request of this batch can see, and
@@ -560,7 +475,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         if (L.cache_table) xtab = as_global((uint64_t*)L.cache_table + (size_t)(region - L.region_base) * NS);
     // Few records: probe and update single buckets in HBM (128 B read + 32 B written per
     // distinct key) instead of moving the 8 KB image both ways.
-    const bool sparse = kSparseOn && RPB == 1 && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
+    const bool sparse = kSparseOn && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
     SparseSrc sp{sparse ? tab : nullptr, xtab, batch_min, false};
     // rebuild the LDS table from registers: linear probing from each key's home
     auto rebuild = [&](const Slot (&img)[NS / 64], const uint64_t (&xim)[NS / 64], const bool (&keep)[NS / 64]) {
@@ -600,43 +515,18 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_hits = 0;
     const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint32_t head = 0, count = 0;                    // ring state (wave-uniform)
     // the whole stream is instantiated once per algorithm (uniform per region), so the
     // compiler hoists nothing of the other algorithm into the hot loop
     auto stream = [&](auto algo, auto spc) {
         constexpr int A = decltype(algo)::value;
         constexpr bool SPX = decltype(spc)::value;
         auto slice = [&](const Rec& r, uint32_t c0) {
+            // every record of the stream is the region's: applied straight from registers
             const uint32_t idx = c0 + lane;
-            if constexpr (RPB == 1) {
-                // the bin is the region: every record is ours, applied straight from registers
-                const Applied ap = wave_apply<Codec, A, SPX>(a, S, L, lane, r, idx < end, idx, base, pad,
-                                                     n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
-                put_res<Res>(a, ap.j, ap.alw, ap.rem);
-                if (TOK) a.tok[ap.j] = ap.tok;
-            } else {
-                const bool mine = idx < end &&
-                    (region_local(r.h, a.shard_bits, L.region_bits) & (RPB - 1)) == rb;
-                const uint64_t bal = __ballot(mine);
-                if (mine) {
-                    const uint32_t k = (head + count + popc_below(bal)) % kRing;
-                    S.ring[k] = r;
-                    S.ring_pos[k] = idx;
-                }
-                count += (uint32_t)__popcll(bal);
-                wave_fence();
-                Applied ap;
-                ap.j = pad; ap.alw = false; ap.rem = kRemError; ap.tok = 0.0;
-                if (count >= 64) {
-                    const uint32_t ri = (head + lane) % kRing;
-                    ap = wave_apply<Codec, A, SPX>(a, S, L, lane, S.ring[ri], true, S.ring_pos[ri], base, pad,
-                                           n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
-                    head = (head + 64) % kRing;
-                    count -= 64;
-                }
-                put_res<Res>(a, ap.j, ap.alw, ap.rem);   // exactly one store per slice
-                if (TOK) a.tok[ap.j] = ap.tok;
-            }
+            const Applied ap = wave_apply<Codec, A, SPX>(a, S, L, lane, r, idx < end, idx, base, pad,
+                                                 n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
+            put_res<Res>(a, ap.j, ap.alw, ap.rem);
+            if (TOK) a.tok[ap.j] = ap.tok;
         };
         // unrolled by kDepth so the prefetch registers rotate without moves (a register move
         // would wait on its load and shrink the effective depth to one slice)
@@ -653,18 +543,8 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
             slice(q3, c0 + 192);
             q3 = fetch(c0 + 64 * kDepth + 192);
         }
-        if constexpr (RPB > 1) {
-            if (count > 0) {
-                const bool v = lane < count;
-                const uint32_t ri = (head + (v ? lane : 0u)) % kRing;
-                const Applied ap = wave_apply<Codec, A, SPX>(a, S, L, lane, S.ring[ri], v, S.ring_pos[ri], base,
-                                                     pad, n_allowed, n_invalid, n_caperr, n_rounds, n_hits, sp);
-                put_res<Res>(a, ap.j, ap.alw, ap.rem);
-                if (TOK) a.tok[ap.j] = ap.tok;
-            }
-        }
     };
-    using SpOn = std::integral_constant<bool, kSparseOn && RPB == 1>;
+    using SpOn = std::integral_constant<bool, kSparseOn>;
     using SpOff = std::integral_constant<bool, false>;
     if (L.algo == kAlgoTB) {
         if (sparse) stream(std::integral_constant<int, kAlgoTB>{}, SpOn{});

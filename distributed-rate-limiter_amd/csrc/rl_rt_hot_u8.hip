@@ -2,7 +2,6 @@
 #include "rl_hot.hpp"
 
 namespace rl {
-template hipError_t hot_chains_t<CodecC, uint8_t>(const RegionArgs&, hipStream_t, hipStream_t);
-template hipError_t regions_combined_t<CodecC, uint8_t>(const RegionArgs&, hipStream_t);
+template hipError_t hot_chains_t<CodecC, uint8_t>(const RegionArgs&, hipStream_t);
 template hipError_t hot_fill_t<CodecC, uint8_t>(const RegionArgs&, hipStream_t);
 }  // namespace rl

@@ -3,5 +3,5 @@
 
 namespace rl {
 template hipError_t region_launch_t<CodecC, uint32_t>(const RegionArgs&, hipStream_t, hipStream_t,
-                                                     hipEvent_t, hipEvent_t, hipStream_t, hipEvent_t);
+                                           hipEvent_t, hipEvent_t);
 }  // namespace rl

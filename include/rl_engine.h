@@ -225,9 +225,8 @@ int  rl_sync(rl_engine* e);
  * measurement-only kernel variants whose results are NOT valid (0 = product path);
  * "hot_threshold" (records per region for the hot-key chains, 0 = off), "route" (two-pass
  * tables: the previous batch's hot regions skip the second partition pass, default 1),
- * "region_order" (largest regions dispatched first, default 1), "sparse_max", "split_hot",
- * "region_walk", "bin_shift", "stage_timing", "debug_regions" and the "*_per_cu" grid
- * sizes. Every setting gives the same decisions. "fail_batches" = k makes the next k batch
+ * "region_order" (largest regions dispatched first, default 1), "sparse_max",
+ * "stage_timing", "debug_regions" and the "*_per_cu" grid sizes. Every setting gives the same decisions. "fail_batches" = k makes the next k batch
  * calls fail with RL_E_DEVICE before enqueuing anything (tests of callers' error paths). */
 int  rl_tune(rl_engine* e, const char* key, int64_t value);
 /* Diagnostics (not needed by callers). "region_times": after a batch run with

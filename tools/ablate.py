@@ -39,7 +39,7 @@ remaining = torch.empty(n, dtype=torch.int64, device=dev)
 variants = args.variants.split("/")
 
 
-DEFAULTS = {"ablate": 0, "bin_shift": 0, "upsweep_per_cu": 0, "scatter_per_cu": 0,
+DEFAULTS = {"ablate": 0, "upsweep_per_cu": 0, "scatter_per_cu": 0,
             "unpermute_per_cu": 0, "hot_threshold": 16384}
 
 

@@ -68,8 +68,10 @@ for b in range(args.batches):
         rr = int(rounds[i])
         cyc = " ".join(f"{x / 1e6:6.2f}" for x in d[i, 4:7])
         w7 = int(d[i, 7])
+        cyc2 = " ".join(f"{x / 1e6:6.2f}" for x in d[i, 8:11])
         what = (f"detail {rr & 0xFFFFFFFF:7d} changed {w7 & 0xFFFFFF:6d} "
-                f"T1 updates {(rr >> 32) & 0xFFFF:6d} HOT Mcyc det/run/T1 {cyc}"
+                f"T1 updates {(rr >> 32) & 0xFFFF:6d} HOT Mcyc det/run/T1 {cyc} pre/pass1/pass2 {cyc2} "
+                f"other-key recs {int(d[i, 11])} prefetched {int(d[i, 12])}"
                 if hot[i] else f"rounds {rr:8d}")
         print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  lim {lim_of[i]} "
               f"recs {int(d[i, 2]):9d} {what}")
