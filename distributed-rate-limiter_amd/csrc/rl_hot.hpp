@@ -143,6 +143,19 @@ __device__ inline int64_t hot_t1_lb(const DevLimiter& L, uint64_t a, uint64_t b,
     return hot_pred_k<ALGO>(L, g - 1, a, b, c, 1) ? T0 : g;
 }
 
+// prev * pw of the sliding-window estimate at `now` (:170-174, rounded as Java rounds) for
+// the key state (a, b, c), off the hot chains' fast paths: a call, so that the compiler cannot
+// hoist the window geometry and its fp64 division into them (inlined, they were computed for
+// every request of every detailed chunk, used or not).
+__device__ __attribute__((noinline)) double sw_prev_weighted(int64_t now, uint64_t a, uint64_t b,
+                                                             uint64_t c, int64_t w, double inv_w) {
+    DevLimiter L{};
+    L.window_ms = w;
+    L.inv_window = inv_w;
+    const SWGeo g = sw_geo(now, L);
+    return (double)sw_get(sw_unpack(a, b, c), g.prev_start, now, w) * g.prev_weight;
+}
+
 // Lane order = arrival order; chunk g of the listed regions -> (region i, chunk c).
 __device__ inline uint32_t hot_region_of(const uint32_t* s_base, uint32_t hc, uint32_t g) {
     uint32_t lo = 0, hi = hc;                        // last i with s_base[i] <= g
@@ -436,7 +449,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0, n_other = 0;
     uint32_t n_changed = 0, n_tk = 0, n_fb = 0;       // debug: changes, [T0, T1) updates,
     uint32_t n_late = 0;                              // detailed chunks starting before T0 / ending past T1
-    uint32_t n_prehit = 0;                            // debug: windows whose records were prefetched
+    uint32_t n_prehit = 0;                            // debug: chunks whose records were prefetched
+    uint32_t n_bisect = 0;                            // debug: SW table entries found by bisection
+    uint64_t cyc_build = 0;                           // debug: SW table builds
     uint64_t cyc_run = 0, cyc_search = 0, cyc_detail = 0, cyc_pass2 = 0;   // debug stamps
     uint64_t cyc_pre = 0, cyc_pass1 = 0;
     bool any_hot = false;
@@ -473,8 +488,10 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         // arithmetic is only evaluated where the table is built, each entry verified there
         // by the exact predicate, :158-180).
         int64_t thr_w = INT64_MIN, thr_c = 0;           // table for window thr_w, counts thr_c + lane
+        int64_t w_cache = INT64_MIN / 2;                 // the window of the last chunk detailed
         int64_t thr1 = 0, thr2 = 0;
         auto thr_build = [&](int64_t W, int64_t C) {     // (W, C wave-uniform; state sa, sb, sc)
+            const uint64_t c_b = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
             const int64_t w = L.window_ms;
             // the state after C - (its count in W) allows inside W: every lane's own count
             SW2 s1 = sw_unpack(sa, sb, sc);
@@ -501,6 +518,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                     else return g;
                 }
                 if ((g == W || !pred(g - 1)) && (g == end || pred(g))) return g;
+                ++n_bisect;
                 int64_t l = W, h = end;                  // pred false below l... true at h
                 while (l < h) {
                     const int64_t m = l + (h - l) / 2;
@@ -512,6 +530,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             thr2 = cnt + 2 <= L.max_permits ? first(2) : end;
             thr_w = W;
             thr_c = C;
+            if (a.dbg) cyc_build += __builtin_amdgcn_s_memtime() - c_b;
         };
         // [T0, T1) for the current state from the table, when it covers it
         auto t1_table = [&](int64_t t0, int64_t& t1) {
@@ -572,6 +591,41 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 // (every earlier pending request is denied and leaves the state alone, Lua
                 // :61-67), so a chunk costs 1 + its allows (the balance is a sequential fp64
                 // recurrence, Lua :56-63)
+                if (std::is_same<Codec, CodecC>::value && !__any(pend && q.op != (uint32_t)kOpAcquire)) {
+                    // acquires only (the common case): tb_step in straight-line code. The
+                    // request time as a double is base + now_rel, exact (integers below 2^53),
+                    // so elapsed = now - last_refill is one exact subtraction of doubles
+                    // (Lua :56), the same value as the integer difference converted
+                    const double td = (double)base + (double)(q.now_ms - base);
+                    const double pd = (double)q.permits;
+                    const double cap = L.capacity, rate = L.rate_per_ms, ttld = (double)L.ttl_ms;
+                    while (__any(pend)) {
+                        const double tok = __longlong_as_double((long long)sa);
+                        const double lastd = (double)(int64_t)sb;
+                        const bool ex = (sc & 1u) != 0;
+                        const double x = tok + (td - lastd) * rate;          // Lua :57-58
+                        const double rf = (!ex || td > lastd + ttld) ? cap : (x < cap ? x : cap);
+                        const bool ok = rf >= pd;                              // Lua :61
+                        const double nt = ok ? rf - pd : rf;
+                        const uint64_t mut = __ballot(pend && ok);
+                        const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
+                        if (pend && lane <= fm) {
+                            oa = ok;
+                            orem = d2l(nt);                                   // {allowed, tokens}
+                            tk = nt;
+                            n_allowed += ok ? 1u : 0u;
+                            pend = false;
+                        }
+                        if (fm < 64u) {                                        // persist (:62-64)
+                            // (the lanes after it: the next round, ~20 instructions, decides
+                            // them; [T0, T1) is derived once the chunk is done)
+                            sa = readlane64((uint64_t)__double_as_longlong(nt), fm);
+                            sb = readlane64((uint64_t)q.now_ms, fm);
+                            sc = 1;
+                            changed = true;
+                        }
+                    }
+                }
                 while (__any(pend)) {
                     Outcome o{};
                     if (pend) o = tb_step(L, q.op, q.permits, q.now_ms, sa, sb, sc);
@@ -616,8 +670,12 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 while (__any(pend)) {
                     const uint32_t f0 = (uint32_t)__builtin_ctzll(__ballot(pend));
                     const int64_t t_f = (int64_t)readlane64((uint64_t)q.now_ms, f0);
-                    int64_t rr;
-                    const int64_t W0 = jdiv(t_f, w, L.inv_window, &rr) * w;     // t_f's window
+                    // t_f's window: the last one seen, or one division
+                    if (!(t_f >= w_cache && t_f - w_cache < w)) {
+                        int64_t rr;
+                        w_cache = jdiv(t_f, w, L.inv_window, &rr) * w;
+                    }
+                    const int64_t W0 = w_cache;
                     // (window membership by compares: no per-request division)
                     const bool in_w = q.now_ms >= W0 && q.now_ms - W0 < w;
                     const bool scan = pend && q.op == (uint32_t)kOpAcquire && in_w &&
@@ -672,8 +730,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                                 if (tab && q.now_ms < v1) rem = 0;
                                 else if (tab && q.now_ms < v2) rem = 1;
                                 else {
-                                    const SWGeo g = sw_geo(q.now_ms, L);
-                                    const double t = (double)sw_get(s0, g.prev_start, q.now_ms, w) * g.prev_weight;
+                                    const double t = sw_prev_weighted(q.now_ms, sa, sb, sc, w, L.inv_window);
                                     const int64_t e = d2l(t + (double)cc);
                                     rem = mx - e > 0 ? mx - e : 0;
                                 }
@@ -683,9 +740,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                                 pend = false;
                             }
                         } else {
-                            const SWGeo g = in ? sw_geo(q.now_ms, L) : SWGeo{};
-                            const int64_t P = in ? sw_get(s0, g.prev_start, q.now_ms, w) : 0;
-                            const double tv = (double)P * g.prev_weight;             // :174, rounded
+                            const double tv = in ? sw_prev_weighted(q.now_ms, sa, sb, sc, w, L.inv_window)
+                                                 : 0.0;                                // :174, rounded
                             auto est = [&](int64_t k) { return d2l(tv + (double)(C0 + k)); };
                             int64_t K = -1;
                             if (in) {
@@ -978,6 +1034,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     for (int off = 32; off > 0; off >>= 1) {
         touched += __shfl_xor(touched, off, 64);
         used += __shfl_xor(used, off, 64);
+        n_bisect += __shfl_xor(n_bisect, off, 64);
     }
     if (lane == 0) {
         note_fill(a, region, used, n_caperr != 0);
@@ -993,6 +1050,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             d[4] = cyc_detail; d[5] = cyc_run; d[6] = cyc_search;
             d[7] = min((uint64_t)n_changed, (uint64_t)0xFFFFFF) | min((uint64_t)n_late, (uint64_t)0xFFFFFF) << 24;
             d[8] = cyc_pre; d[9] = cyc_pass1; d[10] = cyc_pass2; d[11] = n_other; d[12] = n_prehit;
+            d[13] = cyc_build; d[14] = n_bisect;
         }
     }
 }

@@ -71,7 +71,8 @@ for b in range(args.batches):
         cyc2 = " ".join(f"{x / 1e6:6.2f}" for x in d[i, 8:11])
         what = (f"detail {rr & 0xFFFFFFFF:7d} changed {w7 & 0xFFFFFF:6d} "
                 f"T1 updates {(rr >> 32) & 0xFFFF:6d} HOT Mcyc det/run/T1 {cyc} pre/pass1/pass2 {cyc2} "
-                f"other-key recs {int(d[i, 11])} prefetched {int(d[i, 12])}"
+                f"other-key recs {int(d[i, 11])} prefetched {int(d[i, 12])} build Mcyc {d[i, 13] / 1e6:.2f} "
+                f"bisect lanes {int(d[i, 14])}"
                 if hot[i] else f"rounds {rr:8d}")
         print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  lim {lim_of[i]} "
               f"recs {int(d[i, 2]):9d} {what}")
@@ -83,5 +84,8 @@ for b in range(args.batches):
     ends = (d[nh, 1] - t0) / 100
     for q in ((0.5, 0.9, 0.99, 0.999, 1.0) if nh.any() else ()):
         print(f"   normal regions end quantile {q}: {np.quantile(ends, q):9.1f} us")
+    print(f"   hot: details {int((rounds[hot] & np.uint64(0xFFFFFFFF)).sum())}, changes "
+          f"{int((d[hot, 7] & np.uint64(0xFFFFFF)).sum())}, detail Mcyc {d[hot, 4].sum() / 1e6:.1f}, "
+          f"pass1 Mcyc {d[hot, 9].sum() / 1e6:.1f}")
     print(f"   normal: sum dur {dur[nh].sum() / 1e3:.1f} ms, recs {int(d[nh, 2].sum())}, "
           f"rounds {int(rounds[nh].sum())}")

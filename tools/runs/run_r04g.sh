@@ -1,5 +1,5 @@
 #!/bin/bash
-# SW allow-time table + precise prefetch: region timeline of mixed over 6 batches + hot parity
+# lean TB acquire rounds + SW window cache: region timeline of mixed over 6 batches + hot parity
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u tools/region_debug.py --config mixed_tenants --batches 6 > gpurun_out/rd_r04g.log 2>&1 || { echo "region_debug failed"; tail -20 gpurun_out/rd_r04g.log; exit 1; }
