@@ -120,6 +120,9 @@ struct rl_engine {
     uint32_t* route_list = nullptr;         // [kRouteSlots] table of region ids (kNone = empty)
     uint32_t* route_start = nullptr;        // [kRouteSlots] this batch's routed bins
     uint32_t* route_cnt = nullptr;          // [kRouteSlots]
+    uint32_t solo_threshold = 4096;         // rl_tune("solo_threshold"): records per cache-on SW
+                                            // region for the single-key allow-run pass (0: off)
+    uint32_t* solo_list = nullptr;          // [kSoloMax + 1]: the listed regions, then their count
     uint32_t sparse_max = 96;               // rl_tune("sparse_max"): records per region up to
                                             // which a region probes single buckets; 0 = never
     uint64_t* dbg = nullptr;                // rl_tune("debug_regions"): per-bin stamps
@@ -297,6 +300,7 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     if (rc == RL_OK) rc = dalloc(&e->route_start, kRouteSlots);
     if (rc == RL_OK) rc = dalloc(&e->route_cnt, kRouteSlots);
     if (rc == RL_OK) rc = dalloc(&e->order_meta, kOrderMeta);
+    if (rc == RL_OK) rc = dalloc(&e->solo_list, kSoloMax + 1);
     if (rc == RL_OK && hipMemset(e->route_list, 0xFF, kRouteSlots * sizeof(uint32_t)) != hipSuccess)
         rc = RL_E_DEVICE;
     if (rc != RL_OK) { rl_destroy(e); return rc; }
@@ -323,7 +327,7 @@ extern "C" void rl_destroy(rl_engine* e) {
     }
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
     dfree(e->route_list); dfree(e->route_start); dfree(e->route_cnt);
-    dfree(e->order); dfree(e->order_meta);
+    dfree(e->order); dfree(e->order_meta); dfree(e->solo_list);
     dfree(e->d_stats);
     dfree(e->s_key); dfree(e->s_permits); dfree(e->s_now); dfree(e->s_lim); dfree(e->s_op);
     dfree(e->s_allowed); dfree(e->s_remaining); dfree(e->s_tokens);
@@ -763,6 +767,15 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ra.order = e->order;
         ra.order_prefix = e->order_prefix;
     }
+    if (cache && e->solo_threshold) {
+        // cache-on sliding windows have no hot path: a key's leading allow run in a large
+        // region is decided by a whole workgroup, the rest by its region wave (rl_solo.hip)
+        uint32_t* cnt = e->solo_list + kSoloMax;
+        HIP_OK(hipMemsetAsync(cnt, 0, sizeof(uint32_t), s));
+        HIP_OK(launch_solo_select(rstart, rcount, rend, n_bins, e->solo_threshold, e->d_lims,
+                                  e->d_region_lim, e->solo_list, cnt, s));
+        HIP_OK(launch_solo(ra, wide, res_bytes, (uint32_t*)rstart, (uint32_t*)rcount, e->solo_list, cnt, s));
+    }
     mark(e, 7);
     // hot chains first (side stream), then the regions
     HIP_OK(launch_region(ra, wide, res_bytes, s, e->hstream, e->hot_ev[0], e->hot_ev[1]));
@@ -1048,6 +1061,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
         if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
         e->hot_threshold = (uint32_t)value;
         e->hot_thr_auto = false;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "solo_threshold") == 0) {     // records per region; 0 = off
+        if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
+        e->solo_threshold = (uint32_t)value;
         return RL_OK;
     }
     if (std::strcmp(key, "sparse_max") == 0) {         // records per region; 0 = image mode only

@@ -292,6 +292,17 @@ hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, h
 template <class Codec, class Res> hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs);
 template <class Codec, class Res> hipError_t hot_fill_t(const RegionArgs& a, hipStream_t s);
 hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s);
+// Single-key allow runs of cache-on sliding-window regions (rl_solo.hip): regions with >= thr
+// records are listed (at most kSoloMax), then k_solo decides each one's leading allow run and
+// moves its start (rstart / rcount) past it, before the region stage.
+constexpr uint32_t kSoloMax = 4096;
+constexpr uint32_t kSoloGrid = 256;
+hipError_t launch_solo_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
+                              uint32_t n_bins, uint32_t thr, const DevLimiter* lims,
+                              const uint8_t* region_lim, uint32_t* list, uint32_t* count,
+                              hipStream_t s);
+hipError_t launch_solo(const RegionArgs& a, bool wide, int res_bytes, uint32_t* rstart, uint32_t* rcount,
+                       const uint32_t* list, const uint32_t* count, hipStream_t s);
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s);   // prep, scan, summaries
 hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s);
 hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,

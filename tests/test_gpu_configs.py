@@ -295,3 +295,38 @@ def test_config1_single_key_stream():
         assert_same((np.concatenate(got[0]), np.concatenate(got[1]), None), want[:3],
                     f"config1 x{batches}")
         assert e.stats()["cache_hits"] == 0
+
+
+def test_solo_runs_cache_on():
+    """Cache-on sliding windows: large regions' leading allow runs decided by k_solo
+    (rl_solo.hip) with a low threshold, so that runs end every way the pass allows — a denial,
+    a put reaching max, a cache entry still valid at the batch start, another key, a peek, a
+    window change — over several batches (state and cache words carried in HBM)."""
+    NSV = 1_000_000
+    rng = np.random.default_rng(0x50105)
+    lims = [[rl_amd.SW, 600, 1_000, 0.0, 0, 40], [rl_amd.SW, 100_000, 60_000, 0.0, 0, 50],
+            [rl_amd.SW, 5, 200, 0.0, 0, 300]]
+    n = 400_000
+    t0 = (T0 // 60_000) * 60_000 + 55_000
+    # few keys (large regions), skewed; limiter by key; bursts that cross the limits
+    keys_u = rng.integers(1, 2**63, 40, dtype=np.uint64)
+    kid = np.minimum(rng.zipf(1.6, n) - 1, 39)
+    keys = keys_u[kid]
+    lim = (kid % 3).astype(np.uint16)
+    now = (t0 * NSV + np.sort(rng.integers(0, 9_000 * NSV, n))).astype(np.int64)
+    permits = rng.integers(1, 3, n).astype(np.int32)
+    ops = np.where(rng.random(n) < 0.0005, rl_amd.OP_PEEK, rl_amd.OP_ACQUIRE).astype(np.uint8)
+    want = COracle(lims).run(keys, permits, now, lim, ops, want_tokens=False)
+    for thr in (64, 0):
+        e = rl_amd.Engine(max_batch=1 << 17, capacity=1 << 10)
+        for l in lims:
+            e.add_limiter(*l)
+        e.tune("solo_threshold", thr)
+        got = [[], []]
+        for sl in np.array_split(np.arange(n), 5):
+            a, r, _, st = e.execute(keys[sl], permits[sl], now[sl], lim[sl], ops[sl], want_tokens=False)
+            assert st == rl_amd.RL_OK, rl_amd.strerror(st)
+            got[0].append(a); got[1].append(r)
+        assert_same((np.concatenate(got[0]), np.concatenate(got[1]), None), want[:3], f"solo thr {thr}")
+        e.close()
+    assert 0 < want[0].sum() < n

@@ -10,7 +10,10 @@ average duration and the per-launch HBM-side byte counters, corrected as
   * WRITE_SIZE is exact for streaming stores               -> x 1
 Both counters are taken from their own --pmc pass (they do not fit one pass). They
 count L2 -> fabric traffic, so Infinity-Cache hits are included: the figure is an
-upper bound on HBM bytes.
+upper bound on HBM bytes. The x2 is calibrated for 16-B/lane streaming reads only; the
+engine's 2-B gathers and scattered stores are calibrated by tools/calib_fetch.sh
+(profiles/r04_calib). TCC_EA0_ATOMIC_sum (its own pass) is the L2's fabric-side atomic
+request count (north_star's atomic profile).
 
 usage: tools/pmc_json.py <profile dir> <config name> [--out profiles/pmc_summary.json]
 """
@@ -33,6 +36,16 @@ def stage_of(name: str):
         return "region"
     if "k_unpermute<" in name or "k_unpermute_split<" in name:
         return "unpermute"
+    if "k_unpermute_mid<" in name:
+        return "unpermute_mid"
+    if "k_hot_chains<" in name:
+        return "hot_chains"
+    if "k_hot_summ<" in name:
+        return "hot_summ"
+    if "k_hot_fill<" in name:
+        return "hot_fill"
+    if "k_solo<" in name:
+        return "solo"
     return None
 
 
@@ -52,7 +65,7 @@ def main():
             st[s] = {"kernel": r["Name"], "calls": int(r["Calls"]),
                      "avg_us": float(r["AverageNs"]) / 1e3}
     counters = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in ("fetch", "write", "tcc", "sq"):
+    for f in ("fetch", "write", "tcc", "sq", "atomic"):
         p = f"{base}/{f}/{f}_counter_collection.csv"
         if not os.path.exists(p):
             continue
@@ -70,6 +83,8 @@ def main():
             d["write_bytes"] = mean["WRITE_SIZE"] * 1024
         if "fetch_bytes" in d and "write_bytes" in d:
             d["hbm_bytes_per_launch"] = d["fetch_bytes"] + d["write_bytes"]
+        if "TCC_EA0_ATOMIC_sum" in mean:
+            d["l2_fabric_atomics"] = mean["TCC_EA0_ATOMIC_sum"]
         if "TCC_HIT_sum" in mean and "TCC_MISS_sum" in mean:
             tot = mean["TCC_HIT_sum"] + mean["TCC_MISS_sum"]
             d["l2_hit_rate"] = mean["TCC_HIT_sum"] / tot if tot else None

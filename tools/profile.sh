@@ -19,4 +19,5 @@ run fetch --pmc FETCH_SIZE || exit 1
 run write --pmc WRITE_SIZE || exit 1
 run tcc --pmc TCC_HIT_sum TCC_MISS_sum || exit 1
 run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY || exit 1
+run atomic --pmc TCC_EA0_ATOMIC_sum || exit 1
 echo done
