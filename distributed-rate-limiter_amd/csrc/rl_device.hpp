@@ -66,7 +66,7 @@ struct DevLimiter {          // 96 B, read-only during a batch
     int32_t algo;
     int32_t region_bits;     // k: the limiter has 2^k regions
     uint32_t region_base;    // first global region id
-    uint32_t pad0;
+    uint32_t lflags;         // kLf* (host-derived properties of this limiter's arithmetic)
     int64_t max_permits;
     int64_t window_ms;       // w
     int64_t ttl_ms;          // SW: w (PEXPIRE on INCR); TB: 2w (Lua PEXPIRE)
@@ -78,6 +78,14 @@ struct DevLimiter {          // 96 B, read-only during a batch
     int64_t cache_ttl_ms;    // localCacheTtl (0: no local cache, the parity-mode default)
     double inv_rate;         // TB: 1 / rate_per_ms (first guesses only, never a decision)
 };
+
+// DevLimiter::lflags. The window fraction of :170-171, (double)(now % w) / w, is an IEEE
+// division; for windows up to 2^22 ms the host checks every remainder r in [0, w) and sets
+// kLfPctMul when r * (1/w) rounds to the same double (one multiply), else kLfPctFma when one
+// fma correction of that product does (exact by exhaustion, not by a theorem); otherwise the
+// kernels divide. Negative remainders (now < 0) follow by symmetry of both roundings.
+constexpr uint32_t kLfPctMul = 1u;
+constexpr uint32_t kLfPctFma = 2u;
 
 // One 32-byte slot of a region (HBM and the LDS image).
 //   TB: a = tokens (f64 bits), b = last_refill ms (i64), c = bit0 "bucket exists"
@@ -94,10 +102,10 @@ struct Slot {
 // a slot is FREE iff its four words (and its local-cache word) are all zero; a key is
 // always found before the first free slot of its probe sequence. A slot whose state is
 // dead (no bucket live) but whose words are not all zero is a TOMBSTONE: it keeps the
-// probe chain intact and may be reused by an insert. Whole-region writers (a region
-// loaded as an LDS image, the TTL sweep, state import) rebuild the chain and write dead
-// slots as zeros; sparse region waves (few records) touch single buckets and never
-// create a hole. The only key whose dead state could be all-zero (tag 0 = mix64(0) with
+// probe chain intact and may be reused by an insert. Writers that load a whole region (a
+// region loaded as an LDS image, the TTL sweep, state import) drop dead slots (written as
+// zeros) and relink or rebuild the chain; sparse region waves (few records) touch single
+// buckets and never create a hole. The only key whose dead state could be all-zero (tag 0 = mix64(0) with
 // a deleted token bucket) is written with c = kDeadMark instead, which no live state has
 // (TB: c bit 0 clear = absent bucket; SW: both counts zero).
 constexpr uint64_t kDeadMark = 2;
@@ -115,6 +123,7 @@ constexpr uint32_t kOccUsed = 1u;       // holds a key (live, or a tombstone wit
 constexpr uint32_t kOccTouched = 2u;    // read or written by this batch
 constexpr uint32_t kOccUnloaded = 4u;   // sparse region: bucket not fetched from HBM yet
 constexpr uint32_t kOccTomb = 8u;       // sparse region: dead slot (claimable by an insert)
+constexpr uint32_t kOccDirty = 16u;     // image region: changed by the load (dropped, moved)
 
 // ---------------------------------------------------------------- hashing
 // splitmix64 finaliser: a bijection on u64, so tags identify keys exactly.
@@ -355,6 +364,17 @@ __device__ inline int64_t jdiv(int64_t a, int64_t w, double inv_w, int64_t* rem)
     return q;
 }
 
+// (double)r / w for |r| < w < 2^31 (:170-171), bit-exact (see kLfPctMul).
+__device__ inline double sw_pct(int64_t r, const DevLimiter& L) {
+    const double dr = (double)(int32_t)r;
+    if (L.lflags & kLfPctMul) return dr * L.inv_window;
+    if (L.lflags & kLfPctFma) {
+        const double q = dr * L.inv_window;
+        return __builtin_fma(__builtin_fma(-q, (double)L.window_ms, dr), L.inv_window, q);
+    }
+    return dr / (double)L.window_ms;
+}
+
 // Window geometry of a request (getWindowKey :185-188 for now and now - w).
 struct SWGeo {
     int64_t curr_start, prev_start;
@@ -371,9 +391,25 @@ __device__ inline SWGeo sw_geo(int64_t now, const DevLimiter& L) {
     g.curr_start = q * w;
     // (now - w) / w == now / w - 1 under truncation iff now >= w (near the epoch it differs)
     g.prev_start = now >= w ? g.curr_start - w : jdiv(now - w, w, L.inv_window, &r2) * w;
-    const double pct = (double)r / (double)w;
-    g.prev_weight = 1.0 - pct;
+    g.prev_weight = 1.0 - sw_pct(r, L);
     return g;
+}
+
+// sw_geo for a request of a wave whose window starts near `wref` (wave-uniform: the start of
+// a window of this batch, >= 0, or -1): a request in that window or the next one takes its
+// start and remainder from one subtraction instead of a division.
+__device__ inline SWGeo sw_geo_ref(int64_t now, const DevLimiter& L, int64_t wref) {
+    const int64_t w = L.window_ms;
+    if (wref >= 0 && now >= wref && now - wref < 2 * w && now >= w) {
+        const int64_t d = now - wref;
+        const bool nx = d >= w;
+        SWGeo g;
+        g.curr_start = nx ? wref + w : wref;
+        g.prev_start = g.curr_start - w;              // (now >= w: truncation agrees, see sw_geo)
+        g.prev_weight = 1.0 - sw_pct(nx ? d - w : d, L);
+        return g;
+    }
+    return sw_geo(now, L);
 }
 
 // getCurrentCount (SlidingWindowRateLimiter.java:158-180).

@@ -363,6 +363,19 @@ static int upload_limiters(rl_engine* e) {
     return RL_OK;
 }
 
+// kLfPctMul / kLfPctFma (rl_device.hpp): checked for every remainder of windows up to 2^22 ms.
+static uint32_t pct_flags(int64_t w, double inv) {
+    if (w > (int64_t(1) << 22)) return 0;
+    const double dw = (double)w;
+    bool mul = true, fma = true;
+    for (int64_t r = 1; r < w && (mul || fma); ++r) {
+        const double dr = (double)r, exact = dr / dw, q = dr * inv;
+        if (q != exact) mul = false;
+        if (std::fma(std::fma(-q, dw, dr), inv, q) != exact) fma = false;
+    }
+    return mul ? kLfPctMul : fma ? kLfPctFma : 0u;
+}
+
 extern "C" int rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* c, uint16_t* id) {
     if (!e || !c) return RL_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(e->mu);
@@ -396,6 +409,7 @@ extern "C" int rl_add_limiter_ex(rl_engine* e, const rl_limiter_config* c, uint1
     d.rate_per_ms = c->refill_per_s / 1000.0;        // TokenBucketRateLimiter.java:85
     d.inv_rate = d.rate_per_ms > 0.0 ? 1.0 / d.rate_per_ms : 0.0;
     d.inv_window = 1.0 / (double)c->window_ms;
+    d.lflags = pct_flags(c->window_ms, d.inv_window);
     d.capacity = (double)c->max_permits;
     h.table_bytes = (size_t)(1ULL << k) * kRegionSlots * sizeof(Slot);
     if (dalloc(&h.table, h.table_bytes) != RL_OK) return RL_E_NOMEM;

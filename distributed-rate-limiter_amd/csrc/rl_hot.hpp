@@ -394,6 +394,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 #pragma unroll
         for (uint32_t k = 0; k < NS / 64; ++k) {
             S.occ[lane + 64 * k] = 0;
+            S.pm[lane + 64 * k] = 0;
             img[k] = tab[lane + 64 * k];
         }
         wave_fence();
@@ -454,6 +455,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     uint64_t cyc_build = 0;                           // debug: SW table builds
     uint64_t cyc_run = 0, cyc_search = 0, cyc_detail = 0, cyc_pass2 = 0;   // debug stamps
     uint64_t cyc_pre = 0, cyc_pass1 = 0;
+    uint64_t cyc_sw[4] = {0, 0, 0, 0};                // debug: SW run: setup, greedy, remaining, commit
+    uint32_t n_sw_it = 0;                             // debug: SW greedy steps
     bool any_hot = false;
     auto pass1 = [&](auto algo, const uint32_t kk) {
         constexpr int A = decltype(algo)::value;
@@ -668,6 +671,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 // bucket, near the epoch, a peek or a reset) run the exact step alone.
                 const int64_t w = L.window_ms, mx = L.max_permits;
                 while (__any(pend)) {
+                    const uint64_t c_it = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
                     const uint32_t f0 = (uint32_t)__builtin_ctzll(__ballot(pend));
                     const int64_t t_f = (int64_t)readlane64((uint64_t)q.now_ms, f0);
                     // t_f's window: the last one seen, or one division
@@ -694,27 +698,50 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         int64_t kk = 0, na = 0;
                         bool al = false;
                         uint32_t cur = 0, last = 0;
+                        const uint64_t c_g = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                        if (a.dbg) cyc_sw[0] += c_g - c_it;
+                        const uint64_t inm = __ballot(in);
                         if (small) {
-                            // greedy scan on the table: the na-th allow is the first request
-                            // at or past T_p(C0 + na); rebuilt when the window fills it
+                            // greedy scan on the table, a run of allows and a run of denials
+                            // per step: the na-th allow is the first request at or past
+                            // T_p(C0 + na); rebuilt when the window fills it
                             for (;;) {
                                 if (C0 + na - thr_c > 63) {     // (wave-uniform) table exhausted
                                     thr_build(W0, C0 + na);
                                     ++n_tk;
                                 }
-                                const uint32_t ix = (uint32_t)(C0 + na - thr_c);
-                                const int64_t u1 = (int64_t)readlane64((uint64_t)thr1, ix);
-                                const int64_t u2 = (int64_t)readlane64((uint64_t)thr2, ix);
-                                const bool cnd = in && lane >= cur;
-                                const uint64_t m = __ballot(cnd && q.now_ms >= (q.permits == 1 ? u1 : u2));
-                                if (cnd) kk = na;
-                                if (!m) break;
-                                const uint32_t fa = (uint32_t)__builtin_ctzll(m);
-                                if (lane == fa) al = true;
-                                last = fa;
-                                ++na;
-                                cur = fa + 1;
+                                const uint64_t mine = inm & ~((1ULL << cur) - 1);          // (cur < 64)
+                                if (!mine) break;
+                                ++n_sw_it;
+                                const bool cand = (mine >> lane) & 1u;
+                                // (1) allows: the r-th from cur needs T_p(C0 + na + r)
+                                const uint32_t r = popc_below(mine);
+                                const int64_t ix = C0 + na - thr_c + (int64_t)r;
+                                const bool oot = cand && ix > 63;
+                                const int src = (int)(ix > 63 ? 63 : ix);
+                                const int64_t u1 = shfl64(thr1, src), u2 = shfl64(thr2, src);
+                                const uint64_t failm = __ballot(cand && (oot || q.now_ms < (q.permits == 1 ? u1 : u2)));
+                                const uint32_t f1 = failm ? (uint32_t)__builtin_ctzll(failm) : 64u;
+                                const uint64_t arun = f1 < 64u ? mine & ((1ULL << f1) - 1) : mine;
+                                if (cand && lane < f1) { al = true; kk = na + (int64_t)r; }
+                                if (arun) last = 63u - (uint32_t)__builtin_clzll(arun);
+                                na += (int64_t)__popcll(arun);
+                                if (f1 == 64u) break;
+                                cur = f1;
+                                if ((__ballot(oot) >> f1) & 1u) continue;     // past the table: rebuild
+                                // (2) denials from f1 while t < T_p(C0 + na)
+                                const uint32_t ixd = (uint32_t)(C0 + na - thr_c);
+                                const int64_t d1 = (int64_t)readlane64((uint64_t)thr1, ixd);
+                                const int64_t d2 = (int64_t)readlane64((uint64_t)thr2, ixd);
+                                const bool cand2 = cand && lane >= f1;
+                                const uint64_t okm = __ballot(cand2 && q.now_ms >= (q.permits == 1 ? d1 : d2));
+                                const uint32_t f2 = okm ? (uint32_t)__builtin_ctzll(okm) : 64u;
+                                if (cand2 && lane < f2) kk = na;
+                                if (f2 == 64u) break;
+                                cur = f2;
                             }
+                            const uint64_t c_r = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                            if (a.dbg) cyc_sw[1] += c_r - c_g;
                             // remaining after the request: max - est(C0 + kk (+1)) = the number
                             // of q <= 2 with T_q at or before t; 2 or more: the exact estimate
                             const int64_t cc = C0 + kk + (al ? 1 : 0);
@@ -739,6 +766,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                                 n_allowed += al ? 1u : 0u;
                                 pend = false;
                             }
+                            if (a.dbg) cyc_sw[2] += __builtin_amdgcn_s_memtime() - c_r;
                         } else {
                             const double tv = in ? sw_prev_weighted(q.now_ms, sa, sb, sc, w, L.inv_window)
                                                  : 0.0;                                // :174, rounded
@@ -751,15 +779,25 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                                 if (est(K + 1) + q.permits <= mx) ++K;
                                 if (K < -1) K = -1;
                             }
-                            for (;;) {
-                                const uint64_t m = __ballot(in && lane >= cur && K >= na);
-                                if (in && lane >= cur) kk = na;
-                                if (!m) break;
-                                const uint32_t fa = (uint32_t)__builtin_ctzll(m);
-                                if (lane == fa) al = true;
-                                last = fa;
-                                ++na;
-                                cur = fa + 1;
+                            for (;;) {                    // runs of allows and denials, as above
+                                const uint64_t mine = inm & ~((1ULL << cur) - 1);
+                                if (!mine) break;
+                                ++n_sw_it;
+                                const bool cand = (mine >> lane) & 1u;
+                                const uint32_t r = popc_below(mine);
+                                const uint64_t failm = __ballot(cand && K < na + (int64_t)r);
+                                const uint32_t f1 = failm ? (uint32_t)__builtin_ctzll(failm) : 64u;
+                                const uint64_t arun = f1 < 64u ? mine & ((1ULL << f1) - 1) : mine;
+                                if (cand && lane < f1) { al = true; kk = na + (int64_t)r; }
+                                if (arun) last = 63u - (uint32_t)__builtin_clzll(arun);
+                                na += (int64_t)__popcll(arun);
+                                if (f1 == 64u) break;
+                                const bool cand2 = cand && lane >= f1;
+                                const uint64_t okm = __ballot(cand2 && K >= na);
+                                const uint32_t f2 = okm ? (uint32_t)__builtin_ctzll(okm) : 64u;
+                                if (cand2 && lane < f2) kk = na;
+                                if (f2 == 64u) break;
+                                cur = f2;
                             }
                             if (in) {
                                 const int64_t e = est(al ? kk + 1 : kk);             // after the request
@@ -769,6 +807,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                                 pend = false;
                             }
                         }
+                        const uint64_t c_c = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
                         if (na > 0) {
                             const int64_t t_last = (int64_t)readlane64((uint64_t)q.now_ms, last);
                             SWGeo gl{};
@@ -776,6 +815,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                             sw_commit_allows(L, gl, sa, sb, sc, (uint32_t)na, t_last);
                             changed = true;
                         }
+                        if (a.dbg) cyc_sw[3] += __builtin_amdgcn_s_memtime() - c_c;
                     }
                     if (stop < 64u) {
                         // the exact step of request `stop` alone (wave-uniform arithmetic)
@@ -1051,6 +1091,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             d[7] = min((uint64_t)n_changed, (uint64_t)0xFFFFFF) | min((uint64_t)n_late, (uint64_t)0xFFFFFF) << 24;
             d[8] = cyc_pre; d[9] = cyc_pass1; d[10] = cyc_pass2; d[11] = n_other; d[12] = n_prehit;
             d[13] = cyc_build; d[14] = n_bisect;
+            d[15] = cyc_sw[0]; d[16] = cyc_sw[1]; d[17] = cyc_sw[2]; d[18] = cyc_sw[3]; d[19] = n_sw_it;
         }
     }
 }

@@ -80,6 +80,11 @@ __device__ inline uint64_t readlane64(uint64_t v, uint32_t lane) {
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)lane);
 }
 
+__device__ inline int64_t shfl64(int64_t v, int src) {
+    return (int64_t)(((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)v >> 32), src, 64) << 32) |
+                     (uint32_t)__shfl((int)(uint32_t)v, src, 64));
+}
+
 __device__ inline uint64_t ord_key(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ULL; }
 
 // Earliest / latest now_ms of the batch's valid requests. A batch with no valid request

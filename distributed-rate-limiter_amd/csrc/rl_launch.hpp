@@ -168,7 +168,7 @@ __host__ __device__ inline void route_slots(uint32_t region, uint32_t& s1, uint3
     s2 = ((region ^ 0x5BD1E995u) * 0x85EBCA6Bu) >> 21;
 }
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
-constexpr uint32_t kDbgWords = 16;       // debug words per bin
+constexpr uint32_t kDbgWords = 24;       // debug words per bin
 // Batch counters are sharded: one device-scope atomic word sustains only ~88 adds per us
 // (MI355X_MICROARCH.md, rows 'dequeue' / 'fanin'), and every region wave adds to them, so a
 // 1.3M-region batch on ONE set of words serialises for >10 ms. Region waves add to slot

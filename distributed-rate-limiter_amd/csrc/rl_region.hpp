@@ -9,9 +9,10 @@ namespace rl {
 
 // ------------------------------------------------------------------ 4. regions
 // One single-wave workgroup per REGION (a partition bin is one region). The region's 256
-// slots (8 KB) live in the wave's LDS for the whole batch (or, for a sparse region, only the
-// 4-slot buckets its probes reach); the wave streams the region's records in arrival order,
-// kDepth slices of 64 in flight, and applies them 64 at a time. No barriers anywhere.
+// slots (8 KB) live in the wave's LDS for the whole batch, loaded in place (or, for a sparse
+// region, only the 4-slot buckets its probes reach); the wave streams the region's records in
+// arrival order, kDepth slices of 64 in flight, and applies them 64 at a time; the slots the
+// batch touched or changed go back to HBM. No barriers anywhere.
 
 
 struct RegionTable {
@@ -21,6 +22,8 @@ struct RegionTable {
     uint64_t sb[kRegionSlots];
     uint64_t sc[kRegionSlots];
     alignas(16) uint32_t occ[kRegionSlots];   // bit0 occupied, bit1 touched by this batch
+    uint64_t pm[kRegionSlots];                // the lanes of the group in flight holding the
+                                              // slot's key (wave_apply; zero between groups)
 };
 // With a sliding-window local cache (SlidingWindowRateLimiter.java:57-64): every slot also
 // carries its key's cache state (block-until ms, sw_step_cache), moved with the slot.
@@ -51,6 +54,7 @@ struct SparseSrc {
     const RL_GLOBAL uint64_t* xtab;   // local-cache words (nullable)
     int64_t keep;                     // slot_live threshold (keep_from)
     bool long_chain;                  // per lane: a probe went past two used buckets
+    int64_t wref = -1;                // a window start near the stream's requests (SW; uniform)
 };
 
 template <class LdsT>
@@ -71,6 +75,37 @@ __device__ inline void fault_bucket(const SparseSrc& sp, const DevLimiter& L, Ld
         S.tag[p + k] = v[k].tag; S.sa[p + k] = v[k].a; S.sb[p + k] = v[k].b; S.sc[p + k] = v[k].c;
         if constexpr (LdsT::kCache) S.sx[p + k] = x[k];
         S.occ[p + k] = fr ? 0u : lv ? kOccUsed : (kOccUsed | kOccTomb);
+    }
+}
+
+// After an in-place load dropped some slots: a key whose probe sequence from its home now
+// meets a free slot before it moves to the first such slot (the invariant of linear probing:
+// a key sits before the first free slot from its home), until no key moves. Both slots of a
+// move are kOccDirty. A move only shortens its key's probe, so the loop ends.
+template <class LdsT>
+__device__ inline void relink(LdsT& S, uint32_t lane) {
+    constexpr uint32_t NS = kRegionSlots;
+    for (;;) {
+        bool again = false;
+#pragma unroll
+        for (uint32_t i = 0; i < NS / 64; ++i) {
+            const uint32_t s = lane + 64 * i;
+            if (S.occ[s] & kOccUsed) {
+                uint32_t p = slot_home(S.tag[s]);
+                while (p != s && (S.occ[p] & kOccUsed)) p = (p + 1) & (NS - 1);
+                if (p != s) {
+                    again = true;
+                    const uint32_t o = S.occ[p];
+                    if (!(o & kOccUsed) && atomicCAS(&S.occ[p], o, kOccUsed | kOccDirty) == o) {
+                        S.tag[p] = S.tag[s]; S.sa[p] = S.sa[s]; S.sb[p] = S.sb[s]; S.sc[p] = S.sc[s];
+                        if constexpr (LdsT::kCache) S.sx[p] = S.sx[s];
+                        S.occ[s] = kOccDirty;
+                    }
+                }
+            }
+            wave_fence();
+        }
+        if (!__any(again)) break;
     }
 }
 
@@ -182,7 +217,8 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             if (fault != kNone) fault_bucket(sp, L, S, fault);
         }
         wave_fence();
-        const uint32_t expect = cand_tomb ? (kOccUsed | kOccTomb) : 0u;
+        // (a free slot may carry kOccDirty: a slot the in-place load dropped)
+        const uint32_t expect = cand_tomb ? (kOccUsed | kOccTomb) : need && cand != kNone ? (S.occ[cand] & kOccDirty) : 0u;
         if (need && cand != kNone && atomicCAS(&S.occ[cand], expect, kOccUsed) == expect) {
             S.tag[cand] = q.h; S.sa[cand] = 0; S.sb[cand] = 0; S.sc[cand] = 0;
             if constexpr (LdsT::kCache) S.sx[cand] = 0;
@@ -203,14 +239,32 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
     // every earlier one is allowed (the current bucket counts them: :114-116) -> the prefix
     // up to and including the first denied request is final. The longer prefix is taken,
     // so a run of denials or a run of allows costs one round, not one per request.
+    // my key's lanes: one LDS OR per lane into its slot's word, read back, cleared
     const bool one_round = (a.ablate & kAblNoRounds) != 0;
-    const uint64_t peers = one_round ? (1ULL << lane)
-                                     : wave_match((uint32_t)slot, kRegionBits, slot >= 0);
+    uint64_t peers = 1ULL << lane;
+    if (!one_round) {
+        if (slot >= 0) atomicOr((unsigned long long*)&S.pm[slot], 1ULL << lane);
+        wave_fence();
+        if (slot >= 0) peers = S.pm[slot];
+        wave_fence();
+        if (slot >= 0) S.pm[slot] = 0;
+    }
     bool pending = slot >= 0;
     SWGeo geo{};
     uint64_t same_w = 0, elig_m = 0;        // (A): lanes in my window / acquires
     if constexpr (!tb) {
-        if (slot >= 0) geo = sw_geo(q.now_ms, L);
+        // the wave's reference window follows its first request (requests of a region come
+        // in arrival order: it moves about once per window)
+        const uint64_t lm = __ballot(slot >= 0);
+        if (lm) {
+            const int64_t n0 = (int64_t)readlane64((uint64_t)q.now_ms, (uint32_t)__builtin_ctzll(lm));
+            const int64_t w = L.window_ms;
+            if (!(sp.wref >= 0 && n0 >= sp.wref && n0 - sp.wref < 2 * w)) {
+                int64_t rr;
+                sp.wref = n0 >= 0 ? jdiv(n0, w, L.inv_window, &rr) * w : -1;
+            }
+        }
+        if (slot >= 0) geo = sw_geo_ref(q.now_ms, L, sp.wref);
         // window index relative to the wave's first window (2 bits; 3 = "far")
         int64_t wmin = slot >= 0 ? geo.curr_start : INT64_MAX;
         for (int o = 32; o > 0; o >>= 1) {
@@ -251,36 +305,46 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 const uint32_t stop = und ? (uint32_t)__builtin_ctzll(und) : 64u;
                 const bool in = scan && lane < stop;
                 const SW2 s0 = sw_unpack(sa, sb, sc);
-                const int64_t C0 = s0.b1_start == W0 ? (int64_t)s0.b1_cnt : 0;
+                const uint32_t C0 = s0.b1_start == W0 ? s0.b1_cnt : 0u;
+                const double C0d = (double)C0;
                 double tv = 0.0;
                 int64_t K = -1;
-                auto est = [&](int64_t kk) { return d2l(tv + (double)(C0 + kk)); };
+                // (double)(C0 + kk) as one exact sum of doubles (counts are u32, kk < 2^31)
+                auto est = [&](int64_t kk) { return d2l(tv + (C0d + (double)(int32_t)kk)); };
                 if (in) {
                     const int64_t P = sw_get(s0, geo.prev_start, q.now_ms, w);
-                    tv = (double)P * geo.prev_weight;                      // :174, rounded
-                    K = mx - (int64_t)q.permits - C0 - (int64_t)tv;        // ~ largest k
+                    tv = (double)(uint32_t)P * geo.prev_weight;            // :174, rounded
+                    K = mx - (int64_t)q.permits - (int64_t)C0 - d2l(tv);   // ~ largest k
+                    if (K < -1) K = -1;           // (then no k >= 0 is allowed: est(0) > mx - p)
                     if (K >= 0 && est(K) + q.permits > mx) --K;           // rounding edges
                     if (K >= 0 && est(K) + q.permits > mx) --K;
                     if (est(K + 1) + q.permits <= mx) ++K;
                     if (K < -1) K = -1;
                 }
-                // greedy scan: kk = the key's allows before this request
+                // greedy scan, a run of allows and a run of denials per step: kk = the key's
+                // allows before this request, k = before lane cur (all uniform per key)
                 uint32_t cur = 0, last = 64u;
                 int64_t k = 0, kk = 0;
                 bool al = false, done = !in;
-                for (;;) {
-                    const bool c = in && !done && lane >= cur;
-                    const uint64_t mk = __ballot(c && K >= k) & peers;
-                    if (c) kk = k;
-                    if (!done && mk == 0) done = true;
-                    if (!__any(!done)) break;
-                    if (!done) {
-                        const uint32_t fa = (uint32_t)__builtin_ctzll(mk);
-                        if (lane == fa) al = true;
-                        last = fa;
-                        ++k;
-                        cur = fa + 1;
-                    }
+                const uint64_t inm = __ballot(in);
+                while (__any(!done)) {
+                    const uint64_t mine = done ? 0ULL : peers & inm & ~((1ULL << cur) - 1);  // (cur < 64)
+                    const bool cand = (mine >> lane) & 1u;
+                    // (1) allows while each one so far is: the r-th from cur needs K >= k + r
+                    const uint32_t r = popc_below(mine);
+                    const uint64_t fail = __ballot(cand && K < k + (int64_t)r) & peers;
+                    const uint32_t f1 = fail ? (uint32_t)__builtin_ctzll(fail) : 64u;
+                    const uint64_t arun = f1 < 64u ? mine & ((1ULL << f1) - 1) : mine;
+                    if (cand && lane < f1) { al = true; kk = k + (int64_t)r; }
+                    if (arun) last = 63u - (uint32_t)__builtin_clzll(arun);
+                    k += (int64_t)__popcll(arun);
+                    // (2) denials from f1 while K < k (state unchanged)
+                    const bool cand2 = cand && lane >= f1;
+                    const uint64_t okm = __ballot(cand2 && K >= k) & peers;
+                    const uint32_t f2 = okm ? (uint32_t)__builtin_ctzll(okm) : 64u;
+                    if (cand2 && lane < f2) kk = k;
+                    cur = f2;
+                    if (f2 == 64u) done = true;
                 }
                 if (in) {
                     const int64_t e = est(al ? kk + 1 : kk);                // after the request
@@ -480,7 +544,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     // rebuild the LDS table from registers: linear probing from each key's home
     auto rebuild = [&](const Slot (&img)[NS / 64], const uint64_t (&xim)[NS / 64], const bool (&keep)[NS / 64]) {
 #pragma unroll
-        for (uint32_t i = 0; i < NS / 64; ++i) S.occ[lane + 64 * i] = 0;
+        for (uint32_t i = 0; i < NS / 64; ++i) { S.occ[lane + 64 * i] = 0; S.pm[lane + 64 * i] = 0; }
         wave_fence();
 #pragma unroll
         for (uint32_t i = 0; i < NS / 64; ++i) {
@@ -496,21 +560,27 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     };
     if (sparse) {
 #pragma unroll
-        for (uint32_t i = 0; i < NS / 64; ++i) S.occ[lane + 64 * i] = kOccUnloaded;
+        for (uint32_t i = 0; i < NS / 64; ++i) { S.occ[lane + 64 * i] = kOccUnloaded; S.pm[lane + 64 * i] = 0; }
         wave_fence();
     } else {
-        // load the region, dropping entries no request of this batch can see
-        Slot img[NS / 64];
-        uint64_t xim[NS / 64];
-        bool keep[NS / 64];
+        // load the region in place, dropping entries no request of this batch can see: live
+        // keys keep their slots, so only the slots this batch changes are written back
+        bool cut = false;
 #pragma unroll
         for (uint32_t i = 0; i < NS / 64; ++i) {
-            img[i] = tab[lane + 64 * i];
-            xim[i] = xtab ? xtab[lane + 64 * i] : 0;
+            const uint32_t s = lane + 64 * i;
+            const Slot v = tab[s];
+            const uint64_t x = xtab ? xtab[s] : 0;
+            const bool fr = slot_free(v, x);
+            const bool kp = !fr && slot_live(L, v, batch_min, x);
+            S.occ[s] = kp ? kOccUsed : fr ? 0u : kOccDirty;
+            S.pm[s] = 0;
+            S.tag[s] = v.tag; S.sa[s] = v.a; S.sb[s] = v.b; S.sc[s] = v.c;
+            if constexpr (LdsT::kCache) S.sx[s] = x;
+            cut |= !fr && !kp;
         }
-#pragma unroll
-        for (uint32_t i = 0; i < NS / 64; ++i) keep[i] = slot_live(L, img[i], batch_min, xim[i]);
-        rebuild(img, xim, keep);
+        wave_fence();
+        if (__any(cut)) relink(S, lane);
     }
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_hits = 0;
@@ -556,7 +626,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     wave_fence();
     uint32_t touched = 0;
     for (uint32_t s = lane; s < NS; s += 64) touched += (S.occ[s] & kOccTouched) ? 1u : 0u;
-    bool whole = !sparse;
+    bool whole = false;                              // rebuilt: every slot goes back
     if (sparse && __any(sp.long_chain)) {
         // probe chains have grown long (tombstones accumulate while a region only ever sees
         // few records): fault in the rest of the region (one bucket per lane), keep its live
@@ -579,17 +649,19 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         rebuild(img, xim, keep);
         whole = true;
     }
-    // ---- write the region back: every slot (free ones as zeros), or in a sparse region
-    // only the slots this batch touched
-    uint32_t used = 0;                               // live keys (whole regions only)
-    uint32_t moved = 0;                              // table bytes read + written (sparse)
+    // ---- write the region back: every slot (free ones as zeros) after a rebuild, else only
+    // the slots this batch touched or changed (kOccDirty: dropped, moved by relink)
+    const bool full = !sparse || whole;             // every slot is in LDS
+    uint32_t used = 0;                               // live keys (full regions only)
+    uint32_t moved = 0;                              // table bytes read + written
     const uint32_t xw = xtab ? 8u : 0u;              // local-cache word per slot
     for (uint32_t s = lane; s < NS; s += 64) {
         const uint32_t o = S.occ[s];
-        used += (whole && (o & kOccUsed) && !(o & kOccTomb)) ? 1u : 0u;
-        if (!whole) moved += (!(o & kOccUnloaded) && (s & 3u) == 0 ? 4u * (32u + xw) : 0u) +
-                             ((o & kOccTouched) ? 32u + xw : 0u);
-        if (!whole && !(o & kOccTouched)) continue;
+        const bool wr = whole || (o & (kOccTouched | kOccDirty));
+        used += (full && (o & kOccUsed) && !(o & kOccTomb)) ? 1u : 0u;
+        moved += (sparse ? (!(o & kOccUnloaded) && (s & 3u) == 0 ? 4u * (32u + xw) : 0u) : 32u + xw) +
+                 (wr ? 32u + xw : 0u);
+        if (!wr) continue;
         Slot v{0, 0, 0, 0};
         uint64_t x = 0;
         if (o & kOccUsed) {
@@ -612,8 +684,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     if (lane == 0) {
         note_fill(a, region, used, n_caperr != 0);
         unsigned long long* st = a.stats + (size_t)(blockIdx.x & (kStatSlots - 1)) * kStWords;
-        atomicAdd(st + kStTableBytes, whole ? (unsigned long long)(2u * NS * (32u + xw))
-                                            : (unsigned long long)moved);
+        atomicAdd(st + kStTableBytes, (unsigned long long)moved);
         if (n_allowed) atomicAdd(st + kStAllowed, (unsigned long long)n_allowed);
         if (n_invalid) atomicAdd(st + kStInvalid, (unsigned long long)n_invalid);
         if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);

@@ -72,7 +72,8 @@ for b in range(args.batches):
         what = (f"detail {rr & 0xFFFFFFFF:7d} changed {w7 & 0xFFFFFF:6d} "
                 f"T1 updates {(rr >> 32) & 0xFFFF:6d} HOT Mcyc det/run/T1 {cyc} pre/pass1/pass2 {cyc2} "
                 f"other-key recs {int(d[i, 11])} prefetched {int(d[i, 12])} build Mcyc {d[i, 13] / 1e6:.2f} "
-                f"bisect lanes {int(d[i, 14])}"
+                f"bisect lanes {int(d[i, 14])} SW run Mcyc setup/greedy/rem/commit "
+                f"{' '.join(f'{x / 1e6:.2f}' for x in d[i, 15:19])} greedy steps {int(d[i, 19])}"
                 if hot[i] else f"rounds {rr:8d}")
         print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  lim {lim_of[i]} "
               f"recs {int(d[i, 2]):9d} {what}")
