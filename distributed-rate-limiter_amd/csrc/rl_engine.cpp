@@ -163,6 +163,7 @@ struct rl_engine {
     uint32_t up_per_cu = 0, sc_per_cu = 0, un_per_cu = 0;   // rl_tune("*_per_cu"), 0 = default
     uint32_t sc_split = 1;                  // rl_tune("scatter_split"): k_scatter_split
     uint32_t un_split = 2;                  // rl_tune("unpermute_split"): k_unpermute_split
+    uint32_t mid_xcd = 0;                   // rl_tune("mid_xcd"): k_unpermute_mid blocks XCD-aware (measured slower)
                                             // 0 off, 1 on, 2 two-pass batches (measured faster there)
     bool force_wide = false;                // rl_tune("wide_records"): 32-B records (any time span)
     bool auto_grow = true;                  // !RL_OPT_FIXED_CAPACITY
@@ -809,6 +810,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
     ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate; ua.per_cu = e->un_per_cu;
     ua.split = e->un_split == 1 || (e->un_split == 2 && passes == 2);
+    ua.mid_xcd = e->mid_xcd;
     HIP_OK(launch_unpermute(ua, res_bytes, s));
     mark(e, 9);
     if (e->timing) {
@@ -1062,6 +1064,7 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "scatter_per_cu") == 0) { e->sc_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "scatter_split") == 0) { e->sc_split = value != 0; return RL_OK; }
     if (std::strcmp(key, "unpermute_split") == 0) { e->un_split = (uint32_t)value; return RL_OK; }
+    if (std::strcmp(key, "mid_xcd") == 0) { e->mid_xcd = value ? 1u : 0u; return RL_OK; }
     if (std::strcmp(key, "unpermute_per_cu") == 0) { e->un_per_cu = (uint32_t)value; return RL_OK; }
     if (std::strcmp(key, "debug_regions") == 0) { e->debug_regions = value != 0; return RL_OK; }
     if (std::strcmp(key, "wide_records") == 0) { e->force_wide = value != 0; return RL_OK; }

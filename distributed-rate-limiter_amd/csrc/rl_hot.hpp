@@ -702,43 +702,29 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         if (a.dbg) cyc_sw[0] += c_g - c_it;
                         const uint64_t inm = __ballot(in);
                         if (small) {
-                            // greedy scan on the table, a run of allows and a run of denials
-                            // per step: the na-th allow is the first request at or past
-                            // T_p(C0 + na); rebuilt when the window fills it
+                            // greedy scan on the table: the na-th allow is the first request
+                            // at or past T_p(C0 + na); rebuilt when the window fills it. (One
+                            // step per allow, thresholds by readlane: a chain's allows are
+                            // mostly one per chunk, where allow runs through per-lane table
+                            // reads measured slower.)
                             for (;;) {
                                 if (C0 + na - thr_c > 63) {     // (wave-uniform) table exhausted
                                     thr_build(W0, C0 + na);
                                     ++n_tk;
                                 }
-                                const uint64_t mine = inm & ~((1ULL << cur) - 1);          // (cur < 64)
-                                if (!mine) break;
                                 ++n_sw_it;
-                                const bool cand = (mine >> lane) & 1u;
-                                // (1) allows: the r-th from cur needs T_p(C0 + na + r)
-                                const uint32_t r = popc_below(mine);
-                                const int64_t ix = C0 + na - thr_c + (int64_t)r;
-                                const bool oot = cand && ix > 63;
-                                const int src = (int)(ix > 63 ? 63 : ix);
-                                const int64_t u1 = shfl64(thr1, src), u2 = shfl64(thr2, src);
-                                const uint64_t failm = __ballot(cand && (oot || q.now_ms < (q.permits == 1 ? u1 : u2)));
-                                const uint32_t f1 = failm ? (uint32_t)__builtin_ctzll(failm) : 64u;
-                                const uint64_t arun = f1 < 64u ? mine & ((1ULL << f1) - 1) : mine;
-                                if (cand && lane < f1) { al = true; kk = na + (int64_t)r; }
-                                if (arun) last = 63u - (uint32_t)__builtin_clzll(arun);
-                                na += (int64_t)__popcll(arun);
-                                if (f1 == 64u) break;
-                                cur = f1;
-                                if ((__ballot(oot) >> f1) & 1u) continue;     // past the table: rebuild
-                                // (2) denials from f1 while t < T_p(C0 + na)
-                                const uint32_t ixd = (uint32_t)(C0 + na - thr_c);
-                                const int64_t d1 = (int64_t)readlane64((uint64_t)thr1, ixd);
-                                const int64_t d2 = (int64_t)readlane64((uint64_t)thr2, ixd);
-                                const bool cand2 = cand && lane >= f1;
-                                const uint64_t okm = __ballot(cand2 && q.now_ms >= (q.permits == 1 ? d1 : d2));
-                                const uint32_t f2 = okm ? (uint32_t)__builtin_ctzll(okm) : 64u;
-                                if (cand2 && lane < f2) kk = na;
-                                if (f2 == 64u) break;
-                                cur = f2;
+                                const uint32_t ix = (uint32_t)(C0 + na - thr_c);
+                                const int64_t u1 = (int64_t)readlane64((uint64_t)thr1, ix);
+                                const int64_t u2 = (int64_t)readlane64((uint64_t)thr2, ix);
+                                const bool cnd = in && lane >= cur;
+                                const uint64_t m = __ballot(cnd && q.now_ms >= (q.permits == 1 ? u1 : u2));
+                                if (cnd) kk = na;
+                                if (!m) break;
+                                const uint32_t fa = (uint32_t)__builtin_ctzll(m);
+                                if (lane == fa) al = true;
+                                last = fa;
+                                ++na;
+                                cur = fa + 1;
                             }
                             const uint64_t c_r = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
                             if (a.dbg) cyc_sw[1] += c_r - c_g;
@@ -779,25 +765,19 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                                 if (est(K + 1) + q.permits <= mx) ++K;
                                 if (K < -1) K = -1;
                             }
-                            for (;;) {                    // runs of allows and denials, as above
-                                const uint64_t mine = inm & ~((1ULL << cur) - 1);
-                                if (!mine) break;
-                                ++n_sw_it;
-                                const bool cand = (mine >> lane) & 1u;
-                                const uint32_t r = popc_below(mine);
-                                const uint64_t failm = __ballot(cand && K < na + (int64_t)r);
-                                const uint32_t f1 = failm ? (uint32_t)__builtin_ctzll(failm) : 64u;
-                                const uint64_t arun = f1 < 64u ? mine & ((1ULL << f1) - 1) : mine;
-                                if (cand && lane < f1) { al = true; kk = na + (int64_t)r; }
-                                if (arun) last = 63u - (uint32_t)__builtin_clzll(arun);
-                                na += (int64_t)__popcll(arun);
-                                if (f1 == 64u) break;
-                                const bool cand2 = cand && lane >= f1;
-                                const uint64_t okm = __ballot(cand2 && K >= na);
-                                const uint32_t f2 = okm ? (uint32_t)__builtin_ctzll(okm) : 64u;
-                                if (cand2 && lane < f2) kk = na;
-                                if (f2 == 64u) break;
-                                cur = f2;
+                            {                             // the greedy scan as a fixpoint (wave_apply)
+                                bool x = in && K >= (int64_t)popc_below(inm);
+                                for (;;) {
+                                    ++n_sw_it;
+                                    kk = (int64_t)popc_below(__ballot(x) & inm);
+                                    const bool nx = in && K >= kk;
+                                    if (!__any(nx != x)) break;
+                                    x = nx;
+                                }
+                                al = x;
+                                const uint64_t am = __ballot(al);
+                                na = (int64_t)__popcll(am);
+                                if (am) last = 63u - (uint32_t)__builtin_clzll(am);
                             }
                             if (in) {
                                 const int64_t e = est(al ? kk + 1 : kk);             // after the request

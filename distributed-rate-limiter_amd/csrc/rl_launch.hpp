@@ -225,6 +225,7 @@ struct UnpermArgs {
     uint32_t ablate;
     uint32_t per_cu;           // persistent-grid workgroups per CU (0: default)
     uint32_t split;            // rl_tune("unpermute_split"): gathers and stores in separate waves
+    uint32_t mid_xcd;          // rl_tune("mid_xcd"): k_unpermute_mid's blocks XCD-aware
 };
 
 struct SynthArgs {

@@ -742,9 +742,11 @@ template <class Res>
 __global__ __launch_bounds__(256) void k_unpermute_mid(const uint32_t* __restrict__ pos1,
                                                        const Res* __restrict__ res,
                                                        Res* __restrict__ mid, uint32_t n,
-                                                       const BatchCtl* __restrict__ ctl) {
+                                                       const BatchCtl* __restrict__ ctl, uint32_t xcd) {
     constexpr int B = 8;
-    const uint32_t base = blockIdx.x * (256u * B) + threadIdx.x;
+    // consecutive blocks of j on one XCD: a pass-0 bin's 2^d1 result streams are then read
+    // through one L2 instead of being fetched into all eight
+    const uint32_t base = (xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x) * (256u * B) + threadIdx.x;
     n = min(n, ctl->n_normal);
     if (base >= n) return;
     uint32_t p[B];
@@ -880,7 +882,7 @@ hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s) {
 template <class Res>
 static void unpermute_mid(const UnpermArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_unpermute_mid<Res>, dim3((a.n + 2047) / 2048), dim3(256), 0, s, a.pos1,
-                       (const Res*)a.res, (Res*)a.mid, a.n, a.ctl);
+                       (const Res*)a.res, (Res*)a.mid, a.n, a.ctl, a.mid_xcd);
 }
 
 hipError_t launch_route_ranges(const uint32_t* bin_base, const uint32_t* bin_total, uint32_t lo_bins,

@@ -55,6 +55,7 @@ struct SparseSrc {
     int64_t keep;                     // slot_live threshold (keep_from)
     bool long_chain;                  // per lane: a probe went past two used buckets
     int64_t wref = -1;                // a window start near the stream's requests (SW; uniform)
+    uint32_t n_it = 0, n_probe = 0;   // debug: greedy steps, probe bucket steps (uniform)
 };
 
 template <class LdsT>
@@ -167,6 +168,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
     if (a.ablate & kAblNoProbe) { if (need) slot = (int32_t)home; need = false; }
     for (;;) {
         if (!__any(need)) break;
+        ++sp.n_probe;
         uint32_t cand = kNone, fault = kNone;
         bool cand_tomb = false;
         if (need) {
@@ -316,36 +318,32 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                     tv = (double)(uint32_t)P * geo.prev_weight;            // :174, rounded
                     K = mx - (int64_t)q.permits - (int64_t)C0 - d2l(tv);   // ~ largest k
                     if (K < -1) K = -1;           // (then no k >= 0 is allowed: est(0) > mx - p)
-                    if (K >= 0 && est(K) + q.permits > mx) --K;           // rounding edges
-                    if (K >= 0 && est(K) + q.permits > mx) --K;
-                    if (est(K + 1) + q.permits <= mx) ++K;
-                    if (K < -1) K = -1;
+                    // rounding edges: K is exact when est(K) fits and est(K + 1) does not
+                    if (K >= 0 && est(K) + q.permits > mx) {
+                        --K;
+                        if (K >= 0 && est(K) + q.permits > mx) --K;
+                    } else if (est(K + 1) + q.permits <= mx) {
+                        ++K;
+                    }
                 }
-                // greedy scan, a run of allows and a run of denials per step: kk = the key's
-                // allows before this request, k = before lane cur (all uniform per key)
-                uint32_t cur = 0, last = 64u;
-                int64_t k = 0, kk = 0;
-                bool al = false, done = !in;
-                const uint64_t inm = __ballot(in);
-                while (__any(!done)) {
-                    const uint64_t mine = done ? 0ULL : peers & inm & ~((1ULL << cur) - 1);  // (cur < 64)
-                    const bool cand = (mine >> lane) & 1u;
-                    // (1) allows while each one so far is: the r-th from cur needs K >= k + r
-                    const uint32_t r = popc_below(mine);
-                    const uint64_t fail = __ballot(cand && K < k + (int64_t)r) & peers;
-                    const uint32_t f1 = fail ? (uint32_t)__builtin_ctzll(fail) : 64u;
-                    const uint64_t arun = f1 < 64u ? mine & ((1ULL << f1) - 1) : mine;
-                    if (cand && lane < f1) { al = true; kk = k + (int64_t)r; }
-                    if (arun) last = 63u - (uint32_t)__builtin_clzll(arun);
-                    k += (int64_t)__popcll(arun);
-                    // (2) denials from f1 while K < k (state unchanged)
-                    const bool cand2 = cand && lane >= f1;
-                    const uint64_t okm = __ballot(cand2 && K >= k) & peers;
-                    const uint32_t f2 = okm ? (uint32_t)__builtin_ctzll(okm) : 64u;
-                    if (cand2 && lane < f2) kk = k;
-                    cur = f2;
-                    if (f2 == 64u) done = true;
+                // the greedy scan as a fixpoint: a lane is allowed iff its key's allows before
+                // it (kk) are <= K. Starting from "every earlier one allowed", each step
+                // recounts; the r-th lane of a key is final once its r earlier lanes are, so
+                // the iteration ends at the sequential result after at most (the busiest key's
+                // lanes) steps — one or two when K grows with time, as inside a window
+                const uint64_t my = peers & __ballot(in);
+                bool al = in && K >= (int64_t)popc_below(my);
+                int64_t kk = 0;
+                for (;;) {
+                    ++sp.n_it;
+                    kk = (int64_t)popc_below(__ballot(al) & my);
+                    const bool nal = in && K >= kk;
+                    if (!__any(nal != al)) break;
+                    al = nal;
                 }
+                const uint64_t am = __ballot(al) & peers;
+                const int64_t k = (int64_t)__popcll(am);
+                const uint32_t last = am ? 63u - (uint32_t)__builtin_clzll(am) : 64u;
                 if (in) {
                     const int64_t e = est(al ? kk + 1 : kk);                // after the request
                     r.alw = al;
@@ -376,6 +374,45 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         }
         return r;
     } else {
+    if constexpr (tb) {
+        // Token bucket, acquires only (the common group): tb_step's acquire branch in
+        // straight-line code per round (Lua :56-65; elapsed as one exact integer difference,
+        // times below 2^53). A round decides each key's requests up to its first allow.
+        if (!(a.ablate & kAblNoStep) && !__any(pending && q.op != (uint32_t)kOpAcquire)) {
+            if (pending && (int64_t)q.permits > L.max_permits) {       // :110-116, no state access
+                r.rem = kRemUnknown;
+                pending = false;
+            }
+            const double pd = (double)q.permits, cap = L.capacity, rate = L.rate_per_ms;
+            while (__any(pending)) {
+                ++n_rounds;
+                uint64_t sa = 0, sb = 0, sc = 0;
+                if (pending) { sa = S.sa[slot]; sb = S.sb[slot]; sc = S.sc[slot]; }
+                const int64_t last = (int64_t)sb;
+                const bool ex = (sc & 1u) && !(q.now_ms > last + L.ttl_ms);
+                const double x = __longlong_as_double((long long)sa) + (double)(q.now_ms - last) * rate;
+                const double rf = !ex ? cap : (x < cap ? x : cap);
+                const bool ok = rf >= pd;
+                const double nt = ok ? rf - pd : rf;
+                const uint64_t mut = __ballot(pending && ok) & peers;
+                const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
+                if (pending && lane <= fm) {
+                    if (lane == fm) {
+                        S.sa[slot] = (uint64_t)__double_as_longlong(nt);
+                        S.sb[slot] = (uint64_t)q.now_ms;
+                        S.sc[slot] = 1;
+                    }
+                    r.alw = ok;
+                    r.rem = d2l(nt);
+                    r.tok = nt;
+                    n_allowed += ok ? 1u : 0u;
+                    pending = false;
+                }
+                wave_fence();
+            }
+            return r;
+        }
+    }
     while (__any(pending)) {
         ++n_rounds;
         Outcome o{};
@@ -528,11 +565,11 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     // kDepth slices of the region's stream in flight (issued while the region image loads);
     // the stream is read once (non-temporal)
     constexpr uint32_t kDepth = 4;
+    const uint64_t t_begin = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     auto fetch = [&](uint32_t c) { return ld_rec<kNtRgRec>(recs + min(c + lane, end - 1)); };
     Rec q0 = fetch(start), q1 = fetch(start + 64), q2 = fetch(start + 128), q3 = fetch(start + 192);
 
-    // ---- load the region, dropping entries no request of this batch can see, and
-    // rebuild its open-addressing table (no tombstones ever reach HBM)
+    // ---- the region's slots: the whole image in place, or (sparse) buckets on demand
     RL_GLOBAL Slot* tab = as_global((Slot*)L.table + (size_t)(region - L.region_base) * NS);
     RL_GLOBAL uint64_t* xtab = nullptr;             // the slots' local-cache states
     if constexpr (LdsT::kCache)
@@ -624,6 +661,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         else stream(std::integral_constant<int, kAlgoSW>{}, SpOff{});
     }
     wave_fence();
+    const uint64_t t_stream = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t touched = 0;
     for (uint32_t s = lane; s < NS; s += 64) touched += (S.occ[s] & kOccTouched) ? 1u : 0u;
     bool whole = false;                              // rebuilt: every slot goes back
@@ -694,6 +732,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         if (a.dbg) {
             uint64_t* d = a.dbg + (size_t)bin * kDbgWords;
             d[0] = t_start; d[1] = __builtin_amdgcn_s_memrealtime(); d[2] = cnt; d[3] = n_rounds;
+            d[4] = t_begin; d[5] = t_stream; d[6] = sparse ? 1u : 0u; d[7] = sp.n_it; d[8] = sp.n_probe;
         }
     }
 }

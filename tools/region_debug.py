@@ -90,3 +90,16 @@ for b in range(args.batches):
           f"pass1 Mcyc {d[hot, 9].sum() / 1e6:.1f}")
     print(f"   normal: sum dur {dur[nh].sum() / 1e3:.1f} ms, recs {int(d[nh, 2].sum())}, "
           f"rounds {int(rounds[nh].sum())}")
+    if nh.any():
+        dn = d[nh].astype(np.int64)
+        load = (dn[:, 0] - dn[:, 4]) / 100.0
+        strm = (dn[:, 5] - dn[:, 0]) / 100.0
+        wb = (dn[:, 1] - dn[:, 5]) / 100.0
+        for name, m in (("image", dn[:, 6] == 0), ("sparse", dn[:, 6] == 1)):
+            if m.any():
+                sl = np.maximum(1, (dn[m, 2] + 63) // 64).sum()
+                print(f"   {name} regions {int(m.sum())}: mean us load {load[m].mean():.2f} stream "
+                      f"{strm[m].mean():.2f} write-back {wb[m].mean():.2f}; recs/region "
+                      f"{dn[m, 2].mean():.0f}; total wave-ms {(load[m] + strm[m] + wb[m]).sum() / 1e3:.0f}; "
+                      f"per 64-record slice: rounds {(dn[m, 3] & ((1 << 62) - 1)).sum() / sl:.2f} "
+                      f"greedy steps {dn[m, 7].sum() / sl:.2f} probe passes {dn[m, 8].sum() / sl:.2f}")

@@ -1,0 +1,17 @@
+#!/bin/bash
+# SW greedy as a fixpoint, lean TB acquire rounds: whole GPU suite, default bench line, slice stats
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/t_r04r.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|mismatch" gpurun_out/t_r04r.log | head -20; tail -20 gpurun_out/t_r04r.log; exit 1; }
+grep -E "passed|failed" gpurun_out/t_r04r.log | tail -2
+timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > gpurun_out/b_r04r.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/b_r04r.log; exit 1; }
+tail -1 gpurun_out/b_r04r.log | python -c "
+import json,sys; d=json.loads(sys.stdin.read())
+print('default', '%.3e'%d['value'], 'ms/step %.3f'%d['ms_per_step'], 'frac %.4f'%d['roofline']['frac'], d.get('parity'), d['stage_ms'])
+for x in ('tb_uniform','zipf_1b'): print(x, '%.3e'%d[x]['value'], 'ms %.3f'%d[x]['ms_per_step'], d[x]['parity'], d[x]['stage_ms'])
+print('config1', d['config1']['parity'], '%.3e'%d['config1']['engine_value'])"
+for c in sw_zipf zipf_1b; do
+timeout -k 10 300 python -u tools/region_debug.py --config $c --batches 2 > gpurun_out/rd_${c}_r04r.log 2>&1 || { echo "region_debug failed"; tail -20 gpurun_out/rd_${c}_r04r.log; exit 1; }
+grep -E "^batch 1|regions [0-9]+: mean|quantile 1.0" gpurun_out/rd_${c}_r04r.log | tail -4
+done
+echo done
