@@ -330,3 +330,13 @@ def test_solo_runs_cache_on():
         assert_same((np.concatenate(got[0]), np.concatenate(got[1]), None), want[:3], f"solo thr {thr}")
         e.close()
     assert 0 < want[0].sum() < n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knob", [("scatter_split", 0), ("unpermute_split", 0), ("unpermute_split", 1),
+                                  ("mid_xcd", 1), ("region_order", 0)])
+def test_config_partition_knobs(knob):
+    """Every partition/unpermute variant the engine keeps behind rl_tune stays bit-exact on
+    the two-pass headline table (routing from batch 1): the non-split scatter, the plain and
+    split unpermute on both passes, the XCD-mapped mid gather, the plain dispatch order."""
+    run_config("zipf_1b", 1 << 22, 3, tune=(knob,))
