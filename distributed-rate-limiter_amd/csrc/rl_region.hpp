@@ -228,6 +228,12 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             need = false;
         }
         wave_fence();
+        // a lane that lost the claim to another request of its own key (a new key with several
+        // requests in the group) finds it there without probing again
+        if (need && cand != kNone && (S.occ[cand] & (kOccUsed | kOccTomb)) == kOccUsed && S.tag[cand] == q.h) {
+            slot = (int32_t)cand;
+            need = false;
+        }
     }
     if (failed) {
         r.rem = kRemError;
