@@ -11,8 +11,9 @@ sliding window 1000/min (SlidingWindowRateLimiter.java:158-180), 100M keys Zipf 
 256M-request batches spanning 60 s each. The same JSON line carries configs[1] (token
 bucket cap 50 at 10/s, 1M keys uniform, 64M-request batches; `tb_uniform`), the per-GPU
 share of configs[4] (TB 50@10/s + SW 1000/min, Zipf s=1.1, 125M keys, 2^27 requests per
-step; `zipf_1b`) and configs[0] (the reference's single-key benchmark; `config1`) as extra
-keys, each with its own roofline, CPU baseline and parity check.
+step; `zipf_1b`), the per-GPU share of configs[3] (10 limiters, 125M keys, 2^27 requests per
+step; `mixed_tenants`) and configs[0] (the reference's single-key benchmark; `config1`) as
+extra keys, each with its own roofline, CPU baseline and parity check.
 
 Multi-GPU (torchrun, one rank per GPU): weak scaling. Every rank is a front-end that
 receives its own slice of the global stream; requests are routed to the owner shard
@@ -89,16 +90,78 @@ KEY_BYTES = 32 + 32            # state slot read + written
 
 # Bytes each pipeline kernel must move as designed (its own I/O, per request), for the
 # per-kernel bandwidth fractions; the headline roofline is the whole step's ALGORITHMIC
-# bytes over the whole step's time.
-def kernel_io_bytes(name, n, u, n_lim, res_bytes):
+# bytes over the whole step's time. Pass 1 of a routed two-pass batch
+# partitions only the n_normal records that pass 0 did not route to their final place
+# (DESIGN.md §4 "Hot-region routing"), so its kernels are charged for those alone.
+def kernel_io_bytes(name, n, u, n_lim, res_bytes, n_normal=None):
     lim = 2 if n_lim > 1 else 0
+    nn = n if n_normal is None else n_normal
     return {
         "upsweep0": n * (8 + lim),
         "scatter0": n * (REQ_IN + lim + 16 + 4),          # request in; record 16 + position 4 out
-        "upsweep1": n * 16, "scatter1": n * (16 + 16 + 4),
+        "upsweep1": nn * 16, "scatter1": nn * (16 + 16 + 4),
         "region": n * (16 + res_bytes) + u * KEY_BYTES,   # records in, packed results out, slots
         "unpermute": n * (4 + res_bytes + REQ_OUT),        # positions + gathered results in, decisions out
     }.get(name)
+
+
+# ---- per-GPU HBM footprint (the driver's --gpus 8 run must fit 288 GB per GPU) ----------
+HBM_BYTES_PER_GPU = 288e9              # MI355X_MICROARCH.md: 288 GB HBM3E per GPU
+_TILE, _TILE_THREADS, _DIGIT_BINS = 65536, 512, 1 << 13     # rl_device.hpp kTile / kTileThreads
+_REGION_BYTES = 256 * 32               # kRegionSlots x sizeof(Slot)
+_HOT_MAX, _HOT_CHUNK = 1024, 64        # rl_launch.hpp kHotMax / kHotChunk
+_ROUTER_EXC = 4096                     # rl_router.cpp kExcCap
+
+
+def engine_max_batch(n, ws, router="capi"):
+    """max_batch of a rank's engine in run(): its per-exchange receive capacity."""
+    return n * ws if (ws > 1 and router == "python") else n * min(ws, 2)
+
+
+def hbm_footprint(name, n, ws, steps, warm, router="capi", recv_cap=0, table_scale=1,
+                  parity_tokens=False, pipeline=False):
+    """Device bytes one rank of `bench.py --gpus ws --config name` holds at its peak, from
+    the allocation sizes in rl_engine.cpp (rl_add_limiter_ex, ensure_scratch, ensure_regions,
+    ensure_hot_summ, ensure_hot_mark) and rl_router.cpp (rl_router_create_ex), plus the
+    inputs and outputs run() keeps resident. Tables are counted at their creation size
+    (test_gpu_bench_footprint checks the model against hipMemGetInfo after a run)."""
+    cfg = CONFIGS[name]
+    n_lim = len(cfg["limiters"])
+    req_in = 8 + 8 + 4 + (2 if n_lim > 1 else 0)
+    out = {"inputs": (steps + warm) * n * req_in,
+           "outputs": n * (1 + 8) + (n * 8 if parity_tokens else 0)}
+    cap = engine_max_batch(n, ws, router)
+    rcap = min(recv_cap or cap, cap) if ws > 1 else n
+    # engine scratch: sized to the largest batch it decides (+1/8, at most max_batch)
+    m = rcap if ws > 1 else n
+    sc_n = max(m, min(cap, max(m + m // 8, 1 << 20)))
+    padn = sc_n + _TILE_THREADS
+    per_rec = 16 + 2 + 16 + 4 + 4 + 8 + 8 + 8     # rec0 digit rec1 pos0 pos1 res tok ext
+    tiles = (sc_n + _TILE - 1) // _TILE
+    sets = 2 if pipeline else 1
+    out["engine_scratch"] = sets * (padn * per_rec + _DIGIT_BINS * tiles * 4)
+    # state tables (rl_add_limiter_ex: load <= 0.5 at capacity, whole bins of 8 regions)
+    cap_keys = cfg["capacity"] * ws * table_scale
+    per_shard = -(-cap_keys // ws)
+    regions = 0
+    for _ in cfg["limiters"]:
+        r = max(-(-per_shard * 2 // 256), 1)
+        k = max((r - 1).bit_length(), 3)
+        regions += 1 << k
+    out["tables"] = regions * _REGION_BYTES
+    out["region_arrays"] = sets * regions * 8 + regions * (4 + 4 + 1) + 4 * (regions + 1)
+    l1 = m // _HOT_CHUNK + _HOT_MAX + 1
+    out["hot_summaries"] = (l1 + l1 // 64 + _HOT_MAX + 1) * 8
+    if ws > 1 and router == "capi":
+        ret = lambda t: t * 8 + ws * (8 + 8 + 16 * _ROUTER_EXC)   # ret_bound (rl_router.cpp)
+        send = n * (4 + 16 + 2 + 8 + 4 + 8 + 8) + ret(n)
+        recv = rcap * (16 + 2 + 8 + 4 + 8 + 1 + 8 + 8) + ret(rcap)
+        out["router"] = send + recv
+    elif ws > 1:
+        out["router"] = ws * n * 48            # python router: device exchange buffers (bound)
+    out["total"] = sum(out.values())
+    out["fits_288GB"] = out["total"] <= HBM_BYTES_PER_GPU
+    return out
 
 
 def dist_env():
@@ -108,14 +171,18 @@ def dist_env():
     return ws, rank, local
 
 
-def load_pmc(config_name, kernel):
-    """HBM traffic of the dominant kernel from the committed rocprofv3 PMC summary."""
+def load_pmc(config_name, kernel, batch, world):
+    """HBM traffic per launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_summary.json, tools/pmc_json.py), or None unless that profile was taken on
+    this exact workload: the same config, requests per GPU per step and world size."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None
     try:
-        d = json.load(open(path))
-        k = d.get(config_name, {}).get(kernel)
+        d = json.load(open(path)).get(config_name, {})
+        if d.get("batch") != batch or d.get("world", 1) != world:
+            return None
+        k = d.get(kernel)
         return None if k is None else float(k["hbm_bytes_per_launch"])
     except Exception:
         return None
@@ -199,7 +266,7 @@ def cpu_baseline(cfg, keys, permits, now, lim, sample_n, gpu_allowed, gpu_remain
     gr = gpu_remaining[:n]
     dec_ok = bool(np.array_equal(ga, aT) and np.array_equal(gr, rT)) and ok_1
     bal = None
-    if has_tb:
+    if has_tb and gpu_tokens is not None:
         gt = gpu_tokens[:n]
         m = ~np.isnan(tT)
         bal = bool(np.array_equal(np.isnan(gt), ~m) and
@@ -274,7 +341,10 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
     # at most its receive capacity (min(ws, 2) x n) per exchange round and splits a step
     # into rounds when an owner receives more (a skewed step); the python router hands an
     # owner everything it receives (up to ws x n).
-    cap = n * ws if (ws > 1 and args.router == "python") else n * min(ws, 2)
+    cap = engine_max_batch(n, ws, args.router)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0 = torch.cuda.mem_get_info(dev)[0]
     eng = rl_amd.Engine(device=local, max_batch=cap,
                         capacity=cfg["capacity"] * ws * args.table_scale, stage_timing=False,
                         shard_index=rank, shard_count=ws,
@@ -335,6 +405,7 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
                      None if tokens0 is None else tokens0.cpu().numpy())
     if warm > 1:
         stages = eng.stage_times()
+    warm_stats = eng.stats()          # the batch whose stage times were just read (routed count)
     eng.tune("stage_timing", 1 if args.stage_timing else 0)
     del tokens0
 
@@ -356,6 +427,7 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
         elapsed = float(tt.item())
     st = eng.last_status()
     stats = eng.stats()
+    used = free0 - torch.cuda.mem_get_info(dev)[0]     # this rank's device bytes at the end
     if args.stage_timing:
         stages = eng.stage_times()
     ms_per_step = elapsed / steps * 1e3
@@ -372,11 +444,12 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
     step_s = elapsed / steps
     achieved = algo_bytes * ws / step_s / 1e9             # whole node
     peak = HBM_PEAK_GBS * ws
-    traffic = load_pmc(name, "step")
+    traffic = load_pmc(name, "step", n, ws)
     res_b = eng.result_width()
     kernels = {}
+    n_normal = n - warm_stats["routed"] if warm > 1 else n
     for k, ms in kern.items():
-        io = kernel_io_bytes(k, n, U, n_lim, res_b)
+        io = kernel_io_bytes(k, n, U, n_lim, res_b, n_normal)
         kernels[k] = {"ms": round(ms, 4), "io_bytes": io,
                       "io_frac": None if io is None else round(io / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     dom = max(kern, key=kern.get) if kern else None
@@ -405,7 +478,10 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
         # (slot read + write)) over the whole step's wall time, against 8 TB/s per GPU. The
         # step is one launch sequence of the pipeline kernels; `kernels` breaks it down.
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": traffic, "kernel": "pipeline (one step)",
+                     "frac": achieved / peak, "traffic": traffic,
+                     "traffic_source": None if traffic is None else
+                     f"profiles/pmc_summary.json[{name}] (same config, {n} requests/GPU, world {ws})",
+                     "kernel": "pipeline (one step)",
                      "algorithmic_bytes_per_step": algo_bytes,
                      "bytes_per_request": req_bytes, "distinct_keys_per_step": U,
                      "dominant_kernel": dom, "kernels": kernels},
@@ -414,6 +490,13 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
                                               "capacity_errors", "regions_touched")},
         "status": rl_amd.strerror(st),
     }
+    fp = hbm_footprint(name, n, ws, steps, warm, args.router, args.recv_cap, args.table_scale,
+                       parity_tokens and has_tb, ws == 1 and args.pipeline)
+    out["hbm_footprint_gb"] = {k: (round(v / 1e9, 3) if not isinstance(v, bool) else v)
+                               for k, v in fp.items()}
+    out["hbm_footprint_gb"]["tables_now"] = round(
+        sum(eng.limiter_slots(i) for i in range(n_lim)) * 32 / 1e9, 3)   # after on-demand growth
+    out["hbm_footprint_gb"]["measured"] = round(used / 1e9, 3)           # hipMemGetInfo delta
     if router is not None and hasattr(router, "stats"):
         rs = router.stats()
         out["router"] = {"rounds_per_step": rs["rounds"] / max(1, rs["steps"]),
@@ -435,7 +518,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="requests per GPU per step (override)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
-                    help="N=1: skip the extra tb_uniform / zipf_1b / config1 keys of the line")
+                    help="N=1: skip the extra tb_uniform / zipf_1b / mixed_tenants / config1 keys of the line")
     ap.add_argument("--cpu-sample", type=int, default=1 << 26)
     ap.add_argument("--tune", action="append", default=[],
                     help="engine knob key=value (rl_tune), e.g. hot_threshold=32768")
@@ -469,24 +552,30 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    baseline = rank == 0 and ws == 1 and not args.no_cpu_baseline
+    # CPU baseline + parity on rank 0's slice of batch 0. The global stream is rank-major, so
+    # that slice is the head of the whole trace: the oracle's sequential replay of it alone is
+    # exact at any world size. At N>1 the router returns no token balances (decisions and
+    # remaining are compared).
+    baseline = rank == 0 and not args.no_cpu_baseline
     out, in0, keep0 = run(args.config, args, ws, rank, local, dev, rehearse, args.steps,
-                          args.warmup, parity_tokens=baseline)
+                          args.warmup, parity_tokens=baseline and ws == 1)
     if baseline:
         k0, p0, t0_, l0 = in0
         cb, dec_ok, bal, m = cpu_baseline(CONFIGS[args.config], k0, p0, t0_, l0, args.cpu_sample,
                                           keep0[0], keep0[1], keep0[2])
+        if ws > 1:
+            cb["sample"] += f" (rank 0's slice: the head of the {ws}-rank global stream)"
         out["cpu_baseline"] = cb
         out["parity"] = parity_text(dec_ok, bal, m)
     else:
         out["cpu_baseline"] = None
     del in0
-    if baseline and not args.no_extra:
+    if baseline and ws == 1 and not args.no_extra:
         torch.cuda.empty_cache()
         # BASELINE configs[1] (tb_uniform) and the per-GPU share of configs[4] (zipf_1b: the
         # north-star 1B-key TB + SW trace at 8 GPUs) on the same box, each with its own
         # roofline, CPU baseline and batch-0 parity (TB balances bit-for-bit)
-        for extra in ("tb_uniform", "zipf_1b"):
+        for extra in ("tb_uniform", "zipf_1b", "mixed_tenants"):
             if extra == args.config:
                 continue
             xo, xin0, xkeep0 = run(extra, args, 1, 0, local, dev, False, args.steps,
@@ -494,7 +583,7 @@ def main():
             cbx, dec_x, bal_x, mx = cpu_baseline(CONFIGS[extra], *xin0, args.cpu_sample,
                                                  xkeep0[0], xkeep0[1], xkeep0[2], single_thread=False)
             out[extra] = {k: xo[k] for k in ("value", "unit", "ms_per_step", "config", "stage_ms",
-                                             "batch_stats", "status", "roofline")}
+                                             "batch_stats", "status", "roofline", "hbm_footprint_gb")}
             out[extra]["roofline_frac"] = xo["roofline"]["frac"]
             out[extra]["cpu_baseline"] = cbx
             out[extra]["parity"] = parity_text(dec_x, bal_x, mx)
@@ -504,6 +593,7 @@ def main():
     if rank == 0:
         print(json.dumps(out))
     if ws > 1:
+        dist.barrier()                     # rank 0's CPU baseline ran after the timed steps
         dist.destroy_process_group()
 
 

@@ -612,8 +612,10 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
     const int d0 = passes == 1 ? bitsP : bitsP - bitsP / 2;
     const int d1 = bitsP - d0;
-    // hot-region routing: pass 0 gets kRouteSlots bins beyond the 2^d0 low-digit ones
-    const bool hot_on = e->hot_threshold > 0 && !cache;
+    // hot-region routing: pass 0 gets kRouteSlots bins beyond the 2^d0 low-digit ones. The
+    // hot path is gated per limiter: regions of a limiter with the local cache are never
+    // listed hot (k_hot_select), so they are never routed either; the other limiters keep it.
+    const bool hot_on = e->hot_threshold > 0;
     const bool route = hot_on && e->route && passes == 2 && !e->pipeline &&
                        (1u << d0) + kRouteSlots <= (1u << kMaxDigitBits);
     const uint32_t nb0 = route ? (1u << d0) + kRouteSlots : 1u << d0;
@@ -646,8 +648,6 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
             HIP_OK(hipStreamWaitEvent(ps, e->in_ev, 0));
         }
     }
-    // the hot-key path assumes that a denial never changes state; with a local cache a
-    // denial may (it puts the estimate, SlidingWindowRateLimiter.java:106-108)
     const bool hot = hot_on;
     // records per region for the hot path: scaled with the batch by default (measured per
     // config: sw_zipf best at 65536 for 2^28 requests, zipf_1b at 32768 for 2^27)
@@ -764,7 +764,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         HIP_OK(hipMemsetAsync(hot_count, 0, kHotMetaWords * sizeof(uint32_t), s));
         if (route) HIP_OK(launch_hot_route_list(e->route_list, e->route_cnt, e->hot_list, hot_count, s));
         HIP_OK(launch_hot_select(rstart, rcount, rend, n_bins, hot_thr, e->hot_list,
-                                 hot_count, e->hot_mark, e->epoch, s));
+                                 hot_count, e->hot_mark, e->epoch, cache ? e->d_lims : nullptr,
+                                 e->d_region_lim, s));
         ra.hot_list = e->hot_list; ra.hot_count = hot_count; ra.hot_mark = e->hot_mark;
         ra.epoch = e->epoch;
         ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ;
@@ -784,7 +785,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     }
     if (cache && e->solo_threshold) {
         // cache-on sliding windows have no hot path: a key's leading allow run in a large
-        // region is decided by a whole workgroup, the rest by its region wave (rl_solo.hip)
+        // region is decided by a whole workgroup, the rest by its region wave (rl_solo.hip).
+        // (k_solo_select lists cache-on regions only, which k_hot_select never lists.)
         uint32_t* cnt = e->solo_list + kSoloMax;
         HIP_OK(hipMemsetAsync(cnt, 0, sizeof(uint32_t), s));
         HIP_OK(launch_solo_select(rstart, rcount, rend, n_bins, e->solo_threshold, e->d_lims,
@@ -827,30 +829,63 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     return RL_OK;
 }
 
+// on-demand growth: a limiter whose regions are filling up (or overflowed: then twice)
+// gets twice (four times) the regions before the next batch
+static void apply_growth(rl_engine* e, const unsigned long long (&grow)[4], bool overflowed) {
+    if (!e->auto_grow || !(grow[0] | grow[1] | grow[2] | grow[3])) return;
+    for (size_t li = 0; li < e->lims.size(); ++li) {
+        if (!((grow[li >> 6] >> (li & 63)) & 1ULL)) continue;
+        for (int t = 0; t < (overflowed ? 2 : 1); ++t)
+            if (grow_once(e, li) != RL_OK) break;          // at the table-size limit: stay
+    }
+}
+
+static int status_of(bool invalid, bool cap_err, bool span_overflow) {
+    int st = RL_OK;
+    if (invalid) st = RL_E_INVALID_REQUEST;
+    if (cap_err) st = RL_E_CAPACITY;
+    if (span_overflow) st = RL_E_INVALID_ARG;
+    return st;
+}
+
 static int collect_status(rl_engine* e) {
     HIP_OK(hipStreamSynchronize(e->stream));
     if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
     if (!e->pending_status) return e->last_status;
     e->pending_status = false;
-    const BatchCtl& c = *e->h_ctl;
+    BatchCtl& c = *e->h_ctl;
     e->hot_hint = c.n_hot;
-    int st = RL_OK;
-    if (c.invalid) st = RL_E_INVALID_REQUEST;
-    if (c.cap_err) st = RL_E_CAPACITY;
-    if (c.span_overflow) st = RL_E_INVALID_ARG;
+    const int st = status_of(c.invalid != 0, c.cap_err != 0, c.span_overflow != 0);
     e->last_status = st;
-    // on-demand growth: a limiter whose regions are filling up (or overflowed: then twice)
-    // gets twice (four times) the regions before the next batch
-    if (e->auto_grow && (c.grow[0] | c.grow[1] | c.grow[2] | c.grow[3])) {
-        for (size_t li = 0; li < e->lims.size(); ++li) {
-            if (!((c.grow[li >> 6] >> (li & 63)) & 1ULL)) continue;
-            for (int t = 0; t < (c.cap_err ? 2 : 1); ++t)
-                if (grow_once(e, li) != RL_OK) break;      // at the table-size limit: stay
-        }
-        e->h_ctl->grow[0] = e->h_ctl->grow[1] = e->h_ctl->grow[2] = e->h_ctl->grow[3] = 0;
-    }
+    apply_growth(e, c.grow, c.cap_err != 0);
+    c.grow[0] = c.grow[1] = c.grow[2] = c.grow[3] = 0;
     return st;
 }
+
+namespace rl {
+int engine_status_accum(rl_engine* e, unsigned long long* acc, void* stream) {
+    if (!e || !acc) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    const BatchScratch& B = e->sc[e->pipeline ? e->next_set ^ 1 : 0];   // the last batch's set
+    HIP_OK(launch_status_accum(B.d_ctl, acc, stream ? (hipStream_t)stream : e->stream));
+    return RL_OK;
+}
+
+int engine_status_settle(rl_engine* e, const unsigned long long* acc) {
+    if (!e || !acc) return RL_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
+    // the last batch's own status is part of acc: it must not be collected (grown) again
+    e->pending_status = false;
+    e->hot_hint = e->h_ctl->n_hot;
+    const int st = status_of(acc[0] & 1u, acc[0] & 2u, acc[0] & 4u);
+    e->last_status = st;
+    const unsigned long long grow[4] = {acc[1], acc[2], acc[3], acc[4]};
+    apply_growth(e, grow, (acc[0] & 2u) != 0);
+    return st;
+}
+}  // namespace rl
 
 extern "C" int rl_execute_batch_device(rl_engine* e, size_t n, const uint64_t* key,
                                        const int32_t* permits, const int64_t* now_ns,

@@ -31,15 +31,23 @@ __device__ inline uint32_t bin_records(const uint32_t* rstart, const uint32_t* r
                                        const uint32_t* rend, uint32_t b) {
     return rend ? rend[b] - rstart[b] : rcount[b];
 }
+// The hot path assumes that a denial never changes state; with the local cache a denial
+// puts the estimate (SlidingWindowRateLimiter.java:106-108). Regions of such limiters stay
+// with the region waves (and k_solo); every other limiter of the engine keeps its chains.
+// lims == nullptr: no limiter has the cache.
+__device__ inline bool hot_eligible(const DevLimiter* lims, const uint8_t* region_lim, uint32_t b) {
+    return !lims || lims[region_lim[b]].cache_ttl_ms <= 0;
+}
 
 __global__ __launch_bounds__(256) void k_hot_hist(const uint32_t* rstart, const uint32_t* rcount,
                                                   const uint32_t* rend, uint32_t n_bins,
-                                                  uint32_t threshold, uint32_t* hot_meta) {
+                                                  uint32_t threshold, uint32_t* hot_meta,
+                                                  const DevLimiter* lims, const uint8_t* region_lim) {
     __shared__ uint32_t h[33];
     if (threadIdx.x < 33) h[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    if (b < n_bins) {
+    if (b < n_bins && hot_eligible(lims, region_lim, b)) {
         const uint32_t cnt = bin_records(rstart, rcount, rend, b);
         if (cnt >= threshold && cnt > 0) atomicAdd(&h[31 - __builtin_clz(cnt)], 1u);
     }
@@ -51,7 +59,8 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
                                                     const uint32_t* rend, uint32_t n_bins,
                                                     uint32_t threshold, uint32_t* hot_list,
                                                     uint32_t* hot_meta, uint32_t* hot_mark,
-                                                    uint32_t epoch) {
+                                                    uint32_t epoch, const DevLimiter* lims,
+                                                    const uint8_t* region_lim) {
     __shared__ uint32_t s_thr;
     __shared__ uint32_t s_off[33];                    // list offset of each size class
     // routed regions (k_hot_route_list) hold the first entries of the list
@@ -68,7 +77,7 @@ __global__ __launch_bounds__(256) void k_hot_select(const uint32_t* rstart, cons
     }
     __syncthreads();
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= n_bins) return;
+    if (b >= n_bins || !hot_eligible(lims, region_lim, b)) return;
     const uint32_t cnt = bin_records(rstart, rcount, rend, b);
     if (cnt == 0 || cnt < s_thr) return;
     // largest size class first: the chains' workgroups are dispatched in list order, and the
@@ -221,11 +230,12 @@ hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s) {
 hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
                              uint32_t n_bins, uint32_t threshold, uint32_t* hot_list,
                              uint32_t* hot_count, uint32_t* hot_mark, uint32_t epoch,
-                             hipStream_t s) {
+                             const DevLimiter* lims, const uint8_t* region_lim, hipStream_t s) {
     const dim3 g((n_bins + 255) / 256), b(256);
-    hipLaunchKernelGGL(k_hot_hist, g, b, 0, s, rstart, rcount, rend, n_bins, threshold, hot_count);
+    hipLaunchKernelGGL(k_hot_hist, g, b, 0, s, rstart, rcount, rend, n_bins, threshold, hot_count,
+                       lims, region_lim);
     hipLaunchKernelGGL(k_hot_select, g, b, 0, s, rstart, rcount, rend, n_bins, threshold, hot_list,
-                       hot_count, hot_mark, epoch);
+                       hot_count, hot_mark, epoch, lims, region_lim);
     return hipGetLastError();
 }
 

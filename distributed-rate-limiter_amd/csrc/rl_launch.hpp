@@ -309,7 +309,7 @@ hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStr
 hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, const uint32_t* rend,
                              uint32_t n_bins, uint32_t threshold, uint32_t* hot_list,
                              uint32_t* hot_count, uint32_t* hot_mark, uint32_t epoch,
-                             hipStream_t s);
+                             const DevLimiter* lims, const uint8_t* region_lim, hipStream_t s);
 hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s);
 // Routing: after the pass-0 scan, copy the routed bins' ranges (before pass 1 reuses the scan
 // arrays) and set ctl->n_normal; after the hot selection, list the routed regions first; after
@@ -389,6 +389,9 @@ hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t sta
                               hipStream_t s);
 hipError_t launch_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, int64_t rem,
                              hipStream_t s);
+// acc[0] |= status flags (1 invalid, 2 capacity, 4 span overflow), acc[1..4] |= ctl->grow
+constexpr uint32_t kStatusAccWords = 5;
+hipError_t launch_status_accum(const BatchCtl* ctl, unsigned long long* acc, hipStream_t s);
 
 // internal helpers of rl_engine.cpp for rl_router.cpp (not part of the C-ABI)
 int route_pack_wire_mm(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key,
@@ -397,5 +400,10 @@ int route_pack_wire_mm(rl_engine* e, size_t n, const uint32_t* perm, const uint6
                        uint32_t* nparts, void* stream);
 int engine_device(rl_engine* e);
 size_t engine_max_batch(rl_engine* e);
+// Split router rounds: fold the engine's last batch status into acc on `stream` (after that
+// batch), and later settle the folded status of several batches at a step boundary: the
+// status those batches return together, with the table growth they asked for applied once.
+int engine_status_accum(rl_engine* e, unsigned long long* acc, void* stream);
+int engine_status_settle(rl_engine* e, const unsigned long long* acc_host);
 
 }  // namespace rl

@@ -453,6 +453,20 @@ hipError_t launch_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, i
     return hipGetLastError();
 }
 
+// Router split rounds: fold one engine batch's status flags and growth bits into a
+// router-owned accumulator (kStatusAccWords), so the rounds of a step need no host read.
+__global__ void k_status_accum(const BatchCtl* ctl, unsigned long long* acc) {
+    if (threadIdx.x != 0) return;
+    acc[0] |= (ctl->invalid ? 1ULL : 0ULL) | (ctl->cap_err ? 2ULL : 0ULL) |
+              (ctl->span_overflow ? 4ULL : 0ULL);
+    for (int i = 0; i < 4; ++i) acc[1 + i] |= ctl->grow[i];
+}
+
+hipError_t launch_status_accum(const BatchCtl* ctl, unsigned long long* acc, hipStream_t s) {
+    hipLaunchKernelGGL(k_status_accum, dim3(1), dim3(64), 0, s, ctl, acc);
+    return hipGetLastError();
+}
+
 hipError_t launch_counts_to_header(const uint32_t* counts, uint32_t g, int64_t* hdr, uint32_t stride,
                                    hipStream_t s) {
     hipLaunchKernelGGL(k_counts_to_header, dim3(1), dim3(64), 0, s, counts, g, hdr, stride);

@@ -286,7 +286,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         same_w = ((wi & 1) ? b0 : ~b0) & ((wi & 2) ? b1 : ~b1);
         elig_m = __ballot(slot >= 0 && wi < 3 && q.op == (uint32_t)kOpAcquire);
     }
-    if constexpr (!tb && !CACHE) {
+    if constexpr (!tb) if (!cache_on) {
         // Sliding window: a greedy scan per key instead of one round per state change. Inside
         // the window W0 of a key's first pending request, its acquires only INCR the current
         // bucket (:114-116), so with k allows before it a request's estimate is
@@ -297,7 +297,8 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         // first request of a key the scan cannot take (another window, before the key's newest
         // bucket, near the epoch, a peek or a reset) runs the exact step alone; its later
         // requests go to the next pass. (The rounds below remain for the token bucket, whose
-        // allows are a sequential fp64 recurrence, and for the local cache.)
+        // allows are a sequential fp64 recurrence, and for a limiter with the local cache; a
+        // cache-off sliding window takes the scan in the cache kernel variant too.)
         {
             const int64_t w = L.window_ms, mx = L.max_permits;
             while (__any(pending)) {
@@ -379,7 +380,8 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
             }
         }
         return r;
-    } else {
+    }
+    {
     if constexpr (tb) {
         // Token bucket, acquires only (the common group): tb_step's acquire branch in
         // straight-line code per round (Lua :56-65; elapsed as one exact integer difference,

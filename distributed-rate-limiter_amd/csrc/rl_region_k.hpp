@@ -9,7 +9,7 @@ namespace rl {
 
 template <class Codec, class Res, bool TOK, bool CACHE = false>
 __global__ __launch_bounds__(64, CACHE ? 3 : RL_REGION_MIN_WAVES) void k_regions(RegionArgs a) {
-    if constexpr (CACHE) {                       // some limiter keeps a local cache (no hot path)
+    if constexpr (CACHE) {                       // some limiter keeps a local cache
         __shared__ RegionTableX S;
         region_body_t<Codec, Res, TOK>(a, blockIdx.x, S);
     } else {
@@ -29,7 +29,10 @@ hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, h
         (void)hipEventRecord(e0, s);
         (void)hipStreamWaitEvent(hs, e0, 0);
         (void)hot_chains_t<Codec, Res>(a, hs);
-        if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true>), g, b, 0, s, a);
+        // (a cache-on limiter beside hot ones: its regions run in the cache variant)
+        if (a.cache && a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, true>), g, b, 0, s, a);
+        else if (a.cache) hipLaunchKernelGGL((k_regions<Codec, Res, false, true>), g, b, 0, s, a);
+        else if (a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true>), g, b, 0, s, a);
         else hipLaunchKernelGGL((k_regions<Codec, Res, false>), g, b, 0, s, a);
         (void)hipEventRecord(e1, hs);
         (void)hipStreamWaitEvent(s, e1, 0);

@@ -86,8 +86,11 @@ struct rl_router {
     uint64_t ret_out_cap = 0;
     uint32_t* lost = nullptr;
     int64_t* h_hdr = nullptr;            // pinned copy of hdr
+    unsigned long long* acc = nullptr;   // split rounds: the rounds' engine statuses, folded on
+                                         // device (kStatusAccWords), settled at the next step
     int64_t pub = RL_OK;                 // status this rank publishes in the next header
-    bool pending = false;
+    bool pending = false;                // the last engine batch's status is still to collect
+    bool acc_pending = false;            // acc holds a split step's statuses to settle
     rl_router_stats st{};
 };
 
@@ -109,7 +112,7 @@ extern "C" void rl_router_destroy(rl_router* r) {
     if (r->own) (void)hipStreamSynchronize(r->own);
     void* bufs[] = {r->perm, r->wire_s, r->lim_s, r->hdr2, r->mm_part, r->hdr, r->k_s, r->p_s, r->t_s,
                     r->back_w, r->ret_in, r->dir, r->wire_r, r->lim_r, r->k_r, r->p_r, r->t_r, r->a_r,
-                    r->rem_r, r->packed_r, r->ret_out, r->lost};
+                    r->rem_r, r->packed_r, r->ret_out, r->lost, r->acc};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (r->h_hdr) (void)hipHostFree(r->h_hdr);
@@ -152,7 +155,9 @@ extern "C" int rl_router_create_ex(rl_engine* e, uint32_t world, uint32_t rank, 
     ok = ok && take(&r->wire_r, m * 16) && take(&r->lim_r, m * 2) && take(&r->k_r, m * 8);
     ok = ok && take(&r->p_r, m * 4) && take(&r->t_r, m * 8) && take(&r->a_r, m);
     ok = ok && take(&r->rem_r, m * 8) && take(&r->packed_r, m * 8) && take(&r->ret_out, r->ret_out_cap);
+    ok = ok && take(&r->acc, kStatusAccWords * 8);
     ok = ok && hipMemset(r->lost, 0, 4) == hipSuccess;
+    ok = ok && hipMemset(r->acc, 0, kStatusAccWords * 8) == hipSuccess;
     ok = ok && hipHostMalloc((void**)&r->h_hdr, 2 * (size_t)world * kHdrWords * 8) == hipSuccess;
     if (!ok) { rl_router_destroy(r); return RL_E_NOMEM; }
     r->st.recv_cap = m;
@@ -206,6 +211,25 @@ static int64_t worse(int64_t a, int64_t b) {
     if (b == RL_OK) return a;
     if (fatal(a) != fatal(b)) return fatal(a) ? a : b;
     return std::min(a, b);
+}
+
+// The status of this rank's last step's engine batches (the previous step is complete:
+// everything before the caller's header exchange or finish). One batch: the engine's own
+// collection; a split step: the rounds' statuses folded on device. Either applies the table
+// growth the batches asked for, here at the step boundary and never between two rounds.
+static int64_t settle_pending(rl_router* r) {
+    int64_t st = RL_OK;
+    if (r->pending) { st = worse(st, rl_last_status(r->e)); r->pending = false; }
+    if (r->acc_pending) {
+        unsigned long long h[kStatusAccWords];
+        if (r->stepped && hipEventSynchronize(r->done) != hipSuccess) return RL_E_DEVICE;
+        if (hipMemcpy(h, r->acc, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemset(r->acc, 0, sizeof(h)) != hipSuccess)
+            return RL_E_DEVICE;
+        st = worse(st, engine_status_settle(r->e, h));
+        r->acc_pending = false;
+    }
+    return st;
 }
 
 static uint64_t clampu(int64_t x, uint64_t hi) {
@@ -267,11 +291,17 @@ extern "C" int rl_router_step(rl_router* r, size_t n, const uint64_t* key, const
     // published in the next header; the statuses received now (every rank's batch two steps
     // back) are the same on all ranks, so all fail together
     if (fatal(r->pub)) r->pub = RL_OK;              // delivered: every rank returns it now, once
-    if (r->pending) { r->pub = worse(r->pub, rl_last_status(e)); r->pending = false; }
-    if (worst != RL_OK) return (int)worst;
+    r->pub = worse(r->pub, settle_pending(r));
     // every rank sees every rank's capacities: a mismatch fails all of them here, before
     // any payload (all ranks must derive the same exchange plan)
-    if (cap_mismatch) return RL_E_INVALID_ARG;
+    if (worst != RL_OK || cap_mismatch) {
+        // this step's own requests are not decided: say so in its outputs, so that a caller
+        // that goes on does not read the previous step's decisions as this one's
+        R_OK(launch_fill_value(allowed, remaining, (uint32_t)n, RL_REMAINING_ERROR, s));
+        R_OK(hipEventRecord(r->done, s));
+        r->stepped = true;
+        return worst != RL_OK ? (int)worst : RL_E_INVALID_ARG;
+    }
     // rounds: each owner's incoming stream (sources in rank order = global arrival order)
     // is cut into pieces of at most rcap requests; round k moves piece k of every owner
     uint64_t rounds = 1, m = 0;
@@ -365,10 +395,11 @@ extern "C" int rl_router_step(rl_router* r, size_t n, const uint64_t* key, const
                 local = worse(local, xrc);
                 R_OK(launch_fill_value(r->a_r, r->rem_r, (uint32_t)mk, RL_REMAINING_ERROR, s));
             } else {
-                // this path is rare: the round's data-dependent status is collected right
-                // away (the next round's batch would replace it)
-                const int bst = rl_last_status(e);
-                if (bst != RL_OK) local = worse(local, bst);
+                // the round's data-dependent status is folded on device (the next round's
+                // batch replaces the engine's own) and settled at the next step: no host
+                // synchronisation and no table growth between the rounds' collectives
+                R_RC(engine_status_accum(e, r->acc, s));
+                r->acc_pending = true;
             }
             R_RC(rl_route_fold(e, mk, r->a_r, r->rem_r, r->packed_r, s));
             R_RC(a2av_at(r, r->packed_r, ro.data(), rr.data(), r->back_w, so.data(), sc.data(), 8, s));
@@ -387,7 +418,7 @@ extern "C" int rl_router_finish(rl_router* r) {
     // the last step may still run on the caller's stream (its return all-to-all and the
     // unpack that counts lost remainders): complete it before reading anything
     if (r->stepped) R_OK(hipEventSynchronize(r->done));
-    if (r->pending) { r->pub = worse(r->pub, rl_last_status(r->e)); r->pending = false; }
+    r->pub = worse(r->pub, settle_pending(r));
     uint32_t lost = 0;
     R_OK(hipMemcpy(&lost, r->lost, 4, hipMemcpyDeviceToHost));
     if (lost) R_OK(hipMemset(r->lost, 0, 4));        // counted once: the next steps start clean

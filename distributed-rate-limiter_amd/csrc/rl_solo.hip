@@ -165,7 +165,22 @@ __global__ __launch_bounds__(kSoloThreads) void k_solo(RegionArgs a, uint32_t* r
             if (f == n) {                                 // no region wave for it
                 atomicAdd(st + kStDistinct, 1ULL);
                 atomicAdd(st + kStRegions, 1ULL);
+                s_ok = 0;                                 // (the fill count below)
             }
+        }
+        if (f == n) {
+            // no region wave runs for this region in this batch, so its growth check (the
+            // live keys a region write-back counts, note_fill) is made here: the run's key may
+            // have taken a free or dead slot. Slot s_slot holds the key's new state.
+            __syncthreads();
+            if (t < NS) {
+                const Slot v = tab[t];
+                const uint64_t x = xtab[t];
+                const bool used = t == s_slot || (!slot_free(v, x) && slot_live(L, v, keep_from(a), x));
+                if (used) atomicAdd(&s_ok, 1u);
+            }
+            __syncthreads();
+            if (t == 0) note_fill(a, bin, s_ok, false);
         }
     }
 }

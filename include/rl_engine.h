@@ -408,9 +408,16 @@ int  rl_router_stats_get(rl_router* r, rl_router_stats* out);
 /* tryAcquire over this rank's slice of the global arrival stream (device buffers; the
  * ranks' slices are ordered by rank). Same results as one engine on the concatenated
  * stream. One host synchronisation per step (the header exchange: RCCL takes its
- * per-peer counts on the host). Errors are collective: an engine error on any rank is
- * returned, once, by EVERY rank's step two steps later (or by rl_router_finish); the
- * router then goes on (the failed batch's requests read RL_REMAINING_ERROR). */
+ * per-peer counts on the host). Errors are collective: a fatal engine error on any rank is
+ * returned, once, by EVERY rank's step — the NEXT step for a failure known when the engine
+ * call returns (a launch error, an allocation failure), TWO steps later for a batch's
+ * data-dependent status (collected at the next step's header exchange, published in the
+ * header after it) — or by rl_router_finish. The failed batch's requests read
+ * RL_REMAINING_ERROR. The step that returns a fatal error does not process its own batch:
+ * all n of its outputs read allowed = 0, remaining = RL_REMAINING_ERROR, so a caller that
+ * goes on never mistakes stale decisions for this batch's. The router then goes on.
+ * Non-fatal statuses (RL_E_INVALID_REQUEST) are not returned by a step: rl_router_finish
+ * reports the worst of them since the previous finish. */
 int  rl_router_step(rl_router* r, size_t n, const uint64_t* key_hash, const int32_t* permits,
                     const int64_t* now_ns, const uint16_t* limiter, uint8_t* allowed,
                     int64_t* remaining, void* stream);

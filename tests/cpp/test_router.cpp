@@ -263,6 +263,12 @@ static void loop_engine_fail_case() {
         CHECK(res[rank].step_rc == RL_E_DEVICE);
         CHECK(res[rank].fail_step == fail_at + 1);
         CHECK(res[rank].finish == RL_OK);            // reported once, at the step
+        // the step that returns the error did not decide its own batch: all of its outputs
+        // say so (not the previous step's decisions, still in the caller's buffers)
+        for (size_t i = 0; i < n; ++i) {
+            const size_t l = (size_t)(fail_at + 1) * n + i;
+            CHECK(res[rank].a[l] == 0 && res[rank].r[l] == RL_REMAINING_ERROR);
+        }
     }
     std::printf("engine failure on rank %d at step %d: every rank's step %d returned %d %d %d %d\n",
                 fail_rank, fail_at, res[0].fail_step, res[0].step_rc, res[1].step_rc, res[2].step_rc,

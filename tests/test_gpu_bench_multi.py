@@ -29,7 +29,8 @@ def _bench(*extra, nproc=2):
            os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "3", "--warmup", "1",
            *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, r.stdout[-3000:] + "\n".join(
+        l for l in r.stderr.splitlines() if l.startswith("[rank"))[-6000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     return json.loads(line)
 
@@ -48,3 +49,25 @@ def test_bench_rehearsal_split_rounds():
     assert d["status"] == "ok"
     rt = d["router"]
     assert rt["split_steps"] == 4 and rt["rounds_per_step"] > 2
+
+
+def _bench1(*extra):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "2",
+           "--no-extra", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_bench_footprint_model_matches_device():
+    """bench.hbm_footprint (the model test_bench_model checks at --gpus 8) against the device
+    bytes the run really holds (hipMemGetInfo before the engine and after the timed steps)."""
+    d = _bench1("--config", "zipf_1b", "--batch", str(1 << 23))
+    fp = d["hbm_footprint_gb"]
+    model = fp["total"] - fp["tables"] + fp["tables_now"]
+    assert abs(fp["measured"] - model) <= 0.6 + 0.05 * model, fp
+    # pass-1 kernels are charged for the records pass 1 partitions: no io_frac above 1
+    for k, v in d["roofline"]["kernels"].items():
+        assert v["io_frac"] is None or v["io_frac"] <= 1.0, (k, v)
+    assert d["roofline"]["traffic"] is None          # no profile of this batch size
+    assert d["parity"].startswith("bit-exact")

@@ -310,3 +310,23 @@ def test_hot_chain_launch_smaller_than_hot_list():
         got[0].append(a); got[1].append(r); got[2].append(t)
     want = o.run(*tr)
     assert_same(tuple(np.concatenate(g) for g in got), want, "chain grid")
+
+
+@pytest.mark.parametrize("two_pass", [False, True])
+def test_hot_path_beside_cache_on_limiter(two_pass):
+    """The hot path is gated per limiter (rl_engine.cpp, k_hot_select): a Zipf-hot token
+    bucket keeps its chains — and, on two-pass tables, its pass-0 routing — while a sliding
+    window with the Caffeine local cache (RateLimitConfig.java:37-38, the api limiter of
+    RateLimiterConfig.java:54-55) shares the engine. The cache-on limiter has its own hot key
+    (k_solo + its region wave) and ~8k live keys, under Caffeine's maximumSize(10000)
+    (SlidingWindowRateLimiter.java:60), so the emulation is exact."""
+    lims = [[rl_amd.TB, 50, 60_000, 10.0], [rl_amd.SW, 100, 10_000, 0.0, 0, 50]]
+    tr = hot_trace(31, 1_200_000, 16_000, 0.5, [0, 1], 120_000, permits_max=2, hot_keys=2)
+    kw = dict(capacity=1 << 21) if two_pass else {}
+    got, want, e = run(lims, tr, batches=4, tune={"hot_threshold": 16384}, **kw)
+    assert_same(got, want, f"hot beside cache ({'two' if two_pass else 'one'}-pass)")
+    st = e.stats()
+    assert st["hot_regions"] >= 1, st                 # the TB hot key ran as a chain
+    assert st["cache_hits"] > 0, st                   # and the cache-on limiter was live
+    if two_pass:
+        assert st["routed"] > 0, st                   # its region was routed in pass 0

@@ -24,6 +24,11 @@ import json
 import os
 
 
+# bench.py CONFIGS[...]["batch"] (requests per GPU per step)
+DEFAULT_BATCH = {"tb_uniform": 1 << 26, "sw_zipf": 1 << 28, "mixed_tenants": 1 << 27,
+                 "zipf_1b": 1 << 27}
+
+
 def stage_of(name: str):
     def raw(n):  # second template argument: pass 0 reads the raw request arrays
         args = n.split("<", 1)[1].split(">")[0].split(",")
@@ -56,6 +61,9 @@ def main():
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
         os.path.abspath(__file__))), "profiles", "pmc_summary.json"))
     ap.add_argument("--tag", default="")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="requests per GPU per step of the profiled run (default: the config's)")
+    ap.add_argument("--world", type=int, default=1, help="ranks of the profiled run")
     a = ap.parse_args()
     base = a.prof_dir.rstrip("/")
     st = {}
@@ -108,6 +116,9 @@ def main():
                       "write_bytes": tot["WRITE_SIZE"] * 1024 / steps, "steps": steps}
         st["step"]["hbm_bytes_per_launch"] = st["step"]["fetch_bytes"] + st["step"]["write_bytes"]
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    # bench.py reports `roofline.traffic` only for the workload the profile was taken on
+    st["batch"] = a.batch or DEFAULT_BATCH[a.config]
+    st["world"] = a.world
     out[a.config] = st
     out.setdefault("_meta", {})["note"] = (
         "per-launch means; fetch_bytes = FETCH_SIZE KiB x1024 x2 (gfx950 wide-read "
@@ -118,6 +129,8 @@ def main():
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
     for s, d in sorted(st.items()):
+        if not isinstance(d, dict):
+            continue
         print(f"{s:10s} {d.get('avg_us', 0):9.1f} us  hbm/launch "
               f"{d.get('hbm_bytes_per_launch', 0) / 1e9:.3f} GB  l2hit {d.get('l2_hit_rate') or 0:.2f}")
 
