@@ -110,6 +110,7 @@ HBM_BYTES_PER_GPU = 288e9              # MI355X_MICROARCH.md: 288 GB HBM3E per G
 _TILE, _TILE_THREADS, _DIGIT_BINS = 65536, 512, 1 << 13     # rl_device.hpp kTile / kTileThreads
 _REGION_BYTES = 256 * 32               # kRegionSlots x sizeof(Slot)
 _HOT_MAX, _HOT_CHUNK = 1024, 64        # rl_launch.hpp kHotMax / kHotChunk
+_WALK_TAB_ENTRIES = 1 << 26                # rl_launch.hpp kWalkTabEntries (uint2 each)
 _ROUTER_EXC = 4096                     # rl_router.cpp kExcCap
 
 
@@ -152,6 +153,7 @@ def hbm_footprint(name, n, ws, steps, warm, router="capi", recv_cap=0, table_sca
     out["region_arrays"] = sets * regions * 8 + regions * (4 + 4 + 1) + 4 * (regions + 1)
     l1 = m // _HOT_CHUNK + _HOT_MAX + 1
     out["hot_summaries"] = (l1 + l1 // 64 + _HOT_MAX + 1) * 8
+    out["walk_tables"] = _WALK_TAB_ENTRIES * 8     # allow-walk tables (hot path on)
     if ws > 1 and router == "capi":
         ret = lambda t: t * 8 + ws * (8 + 8 + 16 * _ROUTER_EXC)   # ret_bound (rl_router.cpp)
         send = n * (4 + 16 + 2 + 8 + 4 + 8 + 8) + ret(n)

@@ -45,14 +45,8 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 // 8 waves per tile (2 per SIMD): the scatter is latency-bound at one wave per SIMD, and
 // more workgroups per CU would put more tiles' partial record lines in flight per L2
 // (same-box A/B, tb_uniform: 3.60 -> 3.24 ms/step vs 4 waves per tile).
-#ifndef RL_TILE_THREADS
-#define RL_TILE_THREADS 512
-#endif
-constexpr int kTileThreads = RL_TILE_THREADS;
-#ifndef RL_TILE_ITEMS
-#define RL_TILE_ITEMS 128                          // per-thread items per tile (A/B builds: -DRL_TILE_ITEMS)
-#endif
-constexpr int kTileItems = RL_TILE_ITEMS;
+constexpr int kTileThreads = 512;
+constexpr int kTileItems = 128;                    // per-thread items per tile
 constexpr int kTile = kTileThreads * kTileItems;  // 65536 requests per tile (default)
 constexpr int kMaxDigitBits = 13;                 // <= 8192 bins per pass
 

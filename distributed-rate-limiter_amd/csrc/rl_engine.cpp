@@ -103,6 +103,9 @@ struct rl_engine {
     HotInfo* hot_info = nullptr;            // [kHotMax]
     uint64_t* hot_summ = nullptr;           // [hot_summ_cap][8]
     size_t hot_summ_cap = 0, hot_summ_l1 = 0;
+    uint2* walk_tab = nullptr;              // [kWalkTabEntries] allow-walk tables (hot chains)
+    bool walk = true;                       // rl_tune("walk"): allow walks in the hot chains
+    uint32_t walk_min = kWalkMinAllows;     // rl_tune("walk_min"): fewest expected allows walked
     uint32_t* hot_mark = nullptr;           // [hot_mark_cap] epoch marks per bin
     size_t hot_mark_cap = 0;
     uint32_t epoch = 0;
@@ -327,6 +330,7 @@ extern "C" void rl_destroy(rl_engine* e) {
         if (B.freed) (void)hipEventDestroy(B.freed);
     }
     dfree(e->hot_list); dfree(e->hot_mark); dfree(e->dbg); dfree(e->hot_info); dfree(e->hot_summ);
+    dfree(e->walk_tab);
     dfree(e->route_list); dfree(e->route_start); dfree(e->route_cnt);
     dfree(e->order); dfree(e->order_meta); dfree(e->solo_list);
     dfree(e->d_stats);
@@ -656,6 +660,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (hot) {
         rc = ensure_hot_mark(e, n_bins);
         if (rc == RL_OK) rc = ensure_hot_summ(e, n);
+        if (rc == RL_OK && e->walk && !e->walk_tab) rc = dalloc(&e->walk_tab, kWalkTabEntries);
         if (rc != RL_OK) return rc;
         if (++e->epoch == 0) {                       // marks hold epochs: restart after wrap
             HIP_OK(hipMemsetAsync(e->hot_mark, 0, e->hot_mark_cap * sizeof(uint32_t), s));
@@ -771,6 +776,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ;
         ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 8; ra.hot_total = e->hot_list + kHotMax + kHotTotalOff;
         ra.route_list = e->route_list; ra.route_start = e->route_start; ra.route_cnt = e->route_cnt;
+        ra.walk_tab = e->walk ? e->walk_tab : nullptr;
+        ra.walk_min = e->walk_min;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
     }
     if (e->region_order) {
@@ -1136,6 +1143,15 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "route") == 0) {             // hot-region routing in pass 0
         e->route = value != 0;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "walk") == 0) {              // allow walks of the hot chains
+        e->walk = value != 0;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "walk_min") == 0) {          // keys walked: at least this many allows expected
+        if (value < 0 || value > 0xFFFFFFFFLL) return RL_E_INVALID_ARG;
+        e->walk_min = (uint32_t)value;
         return RL_OK;
     }
     if (std::strcmp(key, "fail_batches") == 0) {      // the next `value` batches fail (RL_E_DEVICE)

@@ -217,11 +217,28 @@ hipError_t launch_route_next(const HotInfo* hot_info, const uint32_t* hot_count,
     return hipGetLastError();
 }
 
+// Allow-walk tables of this batch's walk keys (slots 2 i + k, i < walk_regions listed
+// regions, each walk_stride entries): every entry "none" before k_hot_summ merges the firsts in.
+__global__ __launch_bounds__(256) void k_walk_init(RegionArgs a) {
+    const uint32_t hc = min(a.hot_count[0], kHotMax);
+    const int64_t lo = batch_lo(a.ctl), hi = batch_hi(a.ctl);
+    const size_t n = (size_t)2 * min(hc, walk_regions(lo, hi)) * walk_stride(lo, hi);
+    const uint4 none = make_uint4(kWalkNone, kWalkNone, kWalkNone, kWalkNone);
+    uint4* t = (uint4*)a.walk_tab;                   // (strides are multiples of 64 entries)
+    const size_t stride2 = (size_t)2 * walk_stride(lo, hi);
+    for (size_t k = (size_t)blockIdx.x * 256 + threadIdx.x; k < n / 2; k += (size_t)gridDim.x * 256) {
+        const uint32_t i = (uint32_t)(2 * k / stride2);   // listed region (tables of walked keys only)
+        const HotInfo& f = a.hot_info[i];
+        if (walk_dense(f, a.lims[a.region_lim[f.bin]], lo, hi, a.walk_min)) t[k] = none;
+    }
+}
+
 hipError_t launch_hot_prepare(const RegionArgs& a, bool wide, hipStream_t s) {
     const dim3 gp(persistent_grid(1u << 30, 4));
     if (wide) hipLaunchKernelGGL(k_hot_prep<CodecW>, dim3(kHotMax), dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_hot_prep<CodecC>, dim3(kHotMax), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hot_scan, dim3(1), dim3(1024), 0, s, a);
+    if (a.walk_tab) hipLaunchKernelGGL(k_walk_init, dim3(2048), dim3(256), 0, s, a);
     if (wide) hipLaunchKernelGGL(k_hot_summ<CodecW>, gp, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_hot_summ<CodecC>, gp, dim3(256), 0, s, a);
     return hipGetLastError();

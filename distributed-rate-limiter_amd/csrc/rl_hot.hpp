@@ -156,6 +156,35 @@ __device__ __attribute__((noinline)) double sw_prev_weighted(int64_t now, uint64
     return (double)sw_get(sw_unpack(a, b, c), g.prev_start, now, w) * g.prev_weight;
 }
 
+// Wave-uniform values made visibly so (v_readfirstlane into SGPRs): the chains' control flow
+// on them then compiles to scalar branches instead of exec-mask regions around 64-bit VALU
+// compares, which a lone wave pays for at every step.
+__device__ inline uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ inline int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ inline uint64_t uni(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | (uint64_t)uni((uint32_t)x);
+}
+__device__ inline int64_t uni(int64_t x) { return (int64_t)uni((uint64_t)x); }
+__device__ inline double uni(double x) {
+    return __longlong_as_double((long long)uni((uint64_t)__double_as_longlong(x)));
+}
+__device__ inline HotInfo uni(const HotInfo& f) {
+    HotInfo u;
+    u.tag = uni(f.tag); u.bin = uni(f.bin); u.start = uni(f.start); u.end = uni(f.end);
+    u.n_chunks = uni(f.n_chunks); u.chunk_base = uni(f.chunk_base); u.ok = uni(f.ok);
+    u.n_groups = uni(f.n_groups); u.group_base = uni(f.group_base); u.tag2 = uni(f.tag2);
+    return u;
+}
+__device__ inline DevLimiter uni(const DevLimiter& l) {
+    DevLimiter u;
+    u.algo = uni(l.algo); u.region_bits = uni(l.region_bits); u.region_base = uni(l.region_base);
+    u.lflags = uni(l.lflags); u.max_permits = uni(l.max_permits); u.window_ms = uni(l.window_ms);
+    u.ttl_ms = uni(l.ttl_ms); u.rate_per_ms = uni(l.rate_per_ms); u.capacity = uni(l.capacity);
+    u.table = uni(l.table); u.inv_window = uni(l.inv_window); u.cache_table = uni(l.cache_table);
+    u.cache_ttl_ms = uni(l.cache_ttl_ms); u.inv_rate = uni(l.inv_rate);
+    return u;
+}
+
 // Lane order = arrival order; chunk g of the listed regions -> (region i, chunk c).
 __device__ inline uint32_t hot_region_of(const uint32_t* s_base, uint32_t hc, uint32_t g) {
     uint32_t lo = 0, hi = hc;                        // last i with s_base[i] <= g
@@ -256,6 +285,26 @@ __device__ inline uint32_t wave_max32(uint32_t v) {
     return v;
 }
 
+// A key the walk pays for, from its expected allows e (an upper estimate: TB a full bucket plus
+// the refill over the batch's span; SW the limit per window over the windows the span
+// touches): at least walk_min of them (kWalkMinAllows), so that the chain is long, and at most
+// 2.5 per 64-record chunk: denser keys allow several times per chunk, which the chunk-by-chunk
+// path decides at one detail per chunk.
+__device__ inline bool walk_dense(const HotInfo& f, const DevLimiter& L, int64_t lo, int64_t hi,
+                                  uint32_t walk_min) {
+    const double span = (double)(hi - lo + 1);
+    const double e = L.algo == kAlgoTB ? L.capacity + L.rate_per_ms * span
+                                       : (double)L.max_permits * (span / (double)L.window_ms + 2.0);
+    return e >= (double)walk_min && 2.0 * e <= 5.0 * (double)f.n_chunks;
+}
+
+// Allow walks (hot_chain): is region i's key table built in this batch (slot 2 i + key)?
+__device__ inline bool walk_table_on(const RegionArgs& a, uint32_t i, const HotInfo& f,
+                                     const DevLimiter& L, int64_t lo, int64_t hi) {
+    return a.walk_tab && i < walk_regions(lo, hi) && f.end - f.start < (1u << 31) &&
+           walk_dense(f, L, lo, hi, a.walk_min);
+}
+
 template <class Codec>
 __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
     using Rec = typename Codec::Rec;
@@ -267,6 +316,8 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const Rec* recs = (const Rec*)a.rec;
     const int64_t base = a.ctl->base_ms;
+    const int64_t lo = batch_lo(a.ctl), hi = batch_hi(a.ctl);
+    const uint64_t lanes_below = (1ULL << lane) - 1;
     for (uint32_t gg = blockIdx.x * 4 + wid; gg < total; gg += gridDim.x * 4) {
         const uint32_t i = hot_region_of(s_base, hc, gg);
         const HotInfo f = a.hot_info[i];
@@ -277,6 +328,14 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
         const uint32_t c0 = (gg - s_base[i]) * 64, c1 = min(c0 + 64, f.n_chunks);
         uint64_t gmn[2] = {~0ULL, ~0ULL}, gmx[2] = {0ULL, 0ULL};
         uint32_t gfl[2] = {0u, 0u};                      // flags: special, hot, early, rest
+        // allow-walk table of each key (slot 2 i + k): the first plain acquire of 1 and of at
+        // most 2 permits in each ms, found once per (chunk, ms) and merged by atomicMin over
+        // the chunks. Group flags (word 2, bits 24-25): the key's plain acquires are not in
+        // time order (bit 24, judged against the chunks before in the group: wcarry), or
+        // some ask for more than 2 permits (bit 25); either keeps the chain off the walk.
+        const bool walk_on = walk_table_on(a, i, f, L, lo, hi);
+        int64_t wcarry[2] = {INT64_MIN, INT64_MIN};
+        uint32_t wflag[2] = {0u, 0u};
         auto load = [&](uint32_t c) { return recs[min(f.start + c * kHotChunk + lane, f.end - 1)]; };
         auto chunk = [&](const Rec& r, uint32_t c) {
             const uint32_t j = f.start + c * kHotChunk + lane;
@@ -310,6 +369,26 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
                         mx = wave_max64(plain ? ord_key(q.now_ms) : 0ULL);
                     }
                 }
+                if (walk_on && (k == 0 || two)) {                // (wave-uniform)
+                    const uint64_t pm = __ballot(plain);
+                    if (pm) {
+                        const uint64_t bp = pm & lanes_below;
+                        const int64_t tp = shfl64(q.now_ms, bp ? 63 - __builtin_clzll(bp) : (int)lane);
+                        const bool ooo = plain && (bp ? tp : wcarry[k]) > q.now_ms;
+                        wflag[k] |= (__ballot(ooo) ? 1u : 0u) | (__ballot(plain && q.permits > 2) ? 2u : 0u);
+                        uint2* wt = a.walk_tab + (size_t)(2 * i + k) * walk_stride(lo, hi);
+                        const uint32_t ix = (uint32_t)(q.now_ms - lo), rel = j - f.start;
+                        const uint64_t b1 = __ballot(plain && q.permits == 1) & lanes_below;
+                        const uint64_t b2 = __ballot(plain && q.permits <= 2) & lanes_below;
+                        const int64_t t1 = shfl64(q.now_ms, b1 ? 63 - __builtin_clzll(b1) : (int)lane);
+                        const int64_t t2 = shfl64(q.now_ms, b2 ? 63 - __builtin_clzll(b2) : (int)lane);
+                        if (plain && q.permits == 1 && (!b1 || t1 != q.now_ms))
+                            atomicMin(&wt[ix].x, rel);
+                        if (plain && q.permits <= 2 && (!b2 || t2 != q.now_ms))
+                            atomicMin(&wt[ix].y, rel);
+                        wcarry[k] = (int64_t)readlane64((uint64_t)q.now_ms, 63u - (uint32_t)__builtin_clzll(pm));
+                    }
+                }
                 const uint32_t ns = (uint32_t)__popcll(__ballot(special));
                 const uint32_t nh = (uint32_t)__popcll(__ballot(hot));
                 const uint32_t ne = (uint32_t)__popcll(__ballot(early));
@@ -341,7 +420,8 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const uint64_t gw0 = gmn[k] ^ 0x8000000000000000ULL, gw1 = gmx[k] ^ 0x8000000000000000ULL;
-            const uint64_t gw2 = (gfl[k] & 1u) | ((gfl[k] >> 1 & 1u) << 8) | ((gfl[k] >> 2 & 1u) << 16);
+            const uint64_t gw2 = (gfl[k] & 1u) | ((gfl[k] >> 1 & 1u) << 8) | ((gfl[k] >> 2 & 1u) << 16) |
+                                 ((uint64_t)wflag[k] << 24);
             const uint64_t gw3 = (uint64_t)(gfl[k] >> 3 & 1u) << 8;   // rest: kept through the verdict
             v = lane == 4u * k ? gw0 : lane == 4u * k + 1 ? gw1 : lane == 4u * k + 2 ? gw2 :
                 lane == 4u * k + 3 ? gw3 : v;
@@ -370,12 +450,12 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     if (i >= hc) return;
     // the passes are sequential critical paths beside thousands of normal-region waves
     __builtin_amdgcn_s_setprio(3);
-    const HotInfo f = a.hot_info[i];
+    const HotInfo f = uni(a.hot_info[i]);
     const uint32_t region = f.bin;                    // a bin is one region
-    const DevLimiter L = a.lims[a.region_lim[region]];
-    const int64_t base = a.ctl->base_ms;
-    const int64_t lo = batch_lo(a.ctl);
-    const int64_t hi = batch_hi(a.ctl);
+    const DevLimiter L = uni(a.lims[uni((uint32_t)a.region_lim[region])]);
+    const int64_t base = uni(a.ctl->base_ms);
+    const int64_t lo = uni(batch_lo(a.ctl));
+    const int64_t hi = uni(batch_hi(a.ctl));
     const Rec* recs = (const Rec*)a.rec;
     Res* res = (Res*)a.res;
     const uint32_t pad = a.n_total + lane;
@@ -457,6 +537,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     uint64_t cyc_pre = 0, cyc_pass1 = 0;
     uint64_t cyc_sw[4] = {0, 0, 0, 0};                // debug: SW run: setup, greedy, remaining, commit
     uint32_t n_sw_it = 0;                             // debug: SW greedy steps
+    uint32_t n_walk = 0, n_find = 0, n_enter = 0;     // debug: walked allows, table steps, block loads
+    uint64_t cyc_find = 0, cyc_walk = 0;              // debug: walk cycles (finding / all)
+    uint64_t cyc_close = 0, cyc_allow = 0;            // debug: walk cycles (verdicts / allows)
     bool any_hot = false;
     auto pass1 = [&](auto algo, const uint32_t kk) {
         constexpr int A = decltype(algo)::value;
@@ -467,7 +550,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         // the hot key's state (registers; written to LDS when it changes) and the range
         // [T0, T1) in which every acquire is denied with remaining 0 (whole chunks and groups
         // inside it are decided without being read)
-        uint64_t sa = S.sa[hs], sb = S.sb[hs], sc = S.sc[hs];
+        uint64_t sa = uni(S.sa[hs]), sb = uni(S.sb[hs]), sc = uni(S.sc[hs]);
         // T1 from the closed-form guess verified at g - 1; when the guess overshoots (the
         // check fails), the exact first allowed time by a search on the same arithmetic
         auto t1_of = [&](int64_t t0) {
@@ -897,6 +980,366 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 detail(grp * 64 + fst, mn, mx, ns, todo);
             }
         };
+        // ---- Allow walk. A key at its limit is allowed about once per refill interval (TB) or
+        // per decay step of its estimate (SW); detailing the chunk of every such allow cost a
+        // lone wave ~3.6K cycles (mixed_tenants: ~6000 allows per key and batch). The walk
+        // finds each next allow from the key's state alone: the first ms t >= ts at which the
+        // key's first plain acquire asking for at most q(t) permits exists — q(t) being what
+        // the state grants at t (TB: the refilled balance, Lua :56-61, one lane per ms; SW: the
+        // window's allow-time table, :104) — 64 ms per step with k_hot_summ's per-ms table (the
+        // first acquire of 1 and of at most 2 permits) in registers. Chunks are decided by verdicts k_hot_fill applies: every record
+        // of the key denied under the chunk's state but up to 4 allowed (offsets), the records
+        // after each under the state it leaves; chunks (or whole groups) whose acquires all
+        // precede the first ms the state grants take the chains' remaining-0 verdict. The
+        // verdicts of the cursor's block of 64 chunks are kept in registers and stored when the
+        // cursor leaves it. A chunk holding a peek / reset, a fifth allow, or an allow after which
+        // the next request of the same ms could be allowed too (a burst) is detailed as before.
+        // Needs the key's plain acquires in time order with at most 2 permits (k_hot_summ's group
+        // flags); tools/walk_model.py is a CPU model of this loop.
+        auto walk = [&]() -> bool {
+            if (!walk_table_on(a, i, f, L, lo, hi)) return false;
+            if constexpr (A == kAlgoSW) {
+                if (lo < L.window_ms) return false;           // near the epoch (:170-172)
+                if ((int64_t)sa > lo) return false;           // the state is newer than the batch
+            }
+            auto up64 = [&](int64_t v, uint32_t o) { return shfl64(v, lane >= o ? (int)(lane - o) : (int)lane); };
+            {   // eligibility over the key's groups; any_hot as the group walk sets it
+                int64_t carry = INT64_MIN;
+                for (uint32_t g0 = 0; g0 < f.n_groups; g0 += 64) {
+                    const uint32_t g = g0 + lane;
+                    const bool has = g < f.n_groups;
+                    const uint64_t* sg = grp_at(g) + ow;
+                    const int64_t mn = has ? (int64_t)sg[0] : INT64_MAX;
+                    const int64_t mx = has ? (int64_t)sg[1] : INT64_MIN;
+                    const uint32_t w2 = has ? (uint32_t)sg[2] : 0u;
+                    any_hot |= ((w2 >> 8) & 0xFFu) != 0;
+                    if (__any((w2 >> 24) & 3u)) return false;
+                    int64_t pmx = mx;                         // max over the groups up to mine
+                    for (uint32_t o = 1; o < 64; o <<= 1) {
+                        const int64_t y = up64(pmx, o);
+                        if (lane >= o && y > pmx) pmx = y;
+                    }
+                    int64_t before = up64(pmx, 1);
+                    if (lane == 0) before = INT64_MIN;
+                    if (carry > before) before = carry;
+                    if (__any(mn != INT64_MAX && mn < before)) return false;
+                    const int64_t top = (int64_t)readlane64((uint64_t)pmx, 63);
+                    if (top > carry) carry = top;
+                }
+            }
+            const uint32_t span = (uint32_t)(hi - lo) + 1u;
+            const uint2* wt = a.walk_tab + (size_t)(2 * i + kk) * walk_stride(lo, hi);
+            auto tab = [&](int64_t t) { return wt[min((uint32_t)(t - lo), span - 1u)]; };
+            // the table window: lane l holds ms wb + l (A), wb + 64 + l (B), wb + 128 + l (C, in flight)
+            int64_t wb = lo;
+            uint2 tA = tab(wb + lane), tB = tab(wb + 64 + lane), tC = tab(wb + 128 + lane);
+            // group window: lane l holds group gwb + l's summary (max plain time, flags, rest word)
+            uint32_t gwb = kNone, g_w2 = 0;
+            int64_t g_mx = INT64_MIN;
+            uint64_t g_w3 = 0;
+            auto gwin = [&](uint32_t g) {
+                if ((g & ~63u) == gwb) return;
+                gwb = g & ~63u;
+                const bool has = gwb + lane < f.n_groups;
+                const uint64_t* sg = grp_at(has ? gwb + lane : 0u) + ow;
+                g_mx = has ? (int64_t)sg[1] : INT64_MIN;
+                g_w2 = has ? (uint32_t)sg[2] : 0u;
+                g_w3 = has ? sg[3] : 0ULL;
+            };
+            // the register block: lane l holds chunk cb + l's summary and its pending verdict
+            // (vF: word 3's flags in bits 0-7, the allows' offsets from bit 8 on, 6 bits each)
+            uint32_t cb = kNone, b_w2 = 0, vF = 0;
+            int64_t b_mx = INT64_MIN;
+            uint64_t vA = 0, vB = 0, vC = 0;
+            auto flush = [&]() {
+                const uint32_t c = cb + lane;
+                if (cb != kNone && vF != 0 && c < f.n_chunks && ((b_w2 >> 8) & 0xFFu)) {
+                    uint64_t* sm = summ_at(c) + ow;
+                    sm[0] = vA; sm[1] = vB; sm[2] = vC;
+                    sm[3] = (uint64_t)(vF & 0xFFu) | ((uint64_t)((b_w2 >> 24) & 0xFFu) << 8) |
+                            ((uint64_t)(vF >> 8) << 16);
+                }
+            };
+            // (the block after it is loaded on entry, so that it is in registers when the
+            // cursor gets there)
+            uint32_t nb = kNone, n_w2 = 0;
+            int64_t n_mx = INT64_MIN;
+            auto load_blk = [&](uint32_t b, uint32_t& w2, int64_t& mx) {
+                const uint32_t c = b + lane;
+                const bool has = c < f.n_chunks;
+                const uint64_t* sm = summ_at(has ? c : 0u) + ow;
+                w2 = has ? (uint32_t)sm[2] : 0u;
+                mx = has ? (int64_t)sm[1] : INT64_MIN;
+            };
+            auto enter = [&](uint32_t b) {
+                if (b == cb) return;
+                flush();
+                cb = b;
+                if (b == nb) { b_w2 = n_w2; b_mx = n_mx; }
+                else { load_blk(b, b_w2, b_mx); ++n_enter; }
+                vF = 0;
+                nb = b + 64;
+                load_blk(nb, n_w2, n_mx);
+            };
+            auto cinfo = [&](uint32_t c, uint32_t& w2, int64_t& mxc) {
+                enter(c & ~63u);
+                w2 = (uint32_t)__builtin_amdgcn_readlane((int)b_w2, (int)(c - cb));
+                mxc = (int64_t)readlane64((uint64_t)b_mx, c - cb);
+            };
+            // the verdict of a denied chunk of the register block (this lane's): remaining 0 when
+            // its acquires all precede q1
+            auto deny_fl = [&](int64_t q1) {
+                return b_mx < q1 ? 1u | (((b_w2 >> 16) & 0xFFu) ? 2u : 0u) : 5u;
+            };
+            // chunks [c0, c1) denied under (x0, x1, x2): whole groups outside the register block
+            // whose acquires all precede q1 take group verdicts, 64 groups per store
+            auto deny = [&](uint32_t c0, uint32_t c1, uint64_t x0, uint64_t x1, uint64_t x2, int64_t q1) {
+                while (c0 < c1) {
+                    const uint32_t b = c0 & ~63u;
+                    if (c0 == b && c1 >= b + 64 && b != cb) {
+                        const uint32_t G0 = b / 64, G1 = min(c1 / 64, (b & ~4095u) / 64 + 64);
+                        gwin(G0);
+                        const uint32_t g = gwb + lane;
+                        const bool in = g >= G0 && g < G1;
+                        const uint64_t bad = __ballot(in && !(g_mx < q1 && !(g_w2 & 0xFFu) && g * 64 != cb));
+                        const uint32_t stop = bad ? gwb + (uint32_t)__builtin_ctzll(bad) : G1;
+                        if (in && g < stop && ((g_w2 >> 8) & 0xFFu)) {
+                            uint64_t* sg = grp_at(g) + ow;
+                            sg[0] = x0; sg[1] = x1; sg[2] = x2;
+                            sg[3] = (g_w3 & 0xFF00u) | (((g_w2 >> 16) & 0xFFu) ? 3u : 1u);
+                        }
+                        if (stop > G0) { c0 = stop * 64; continue; }
+                    }
+                    const uint32_t e = min(c1, b + 64);
+                    enter(b);
+                    const uint32_t c = cb + lane;
+                    const uint32_t fl = deny_fl(q1);
+                    if (c >= c0 && c < e) { vA = x0; vB = x1; vC = x2; vF = fl; }
+                    c0 = e;
+                }
+            };
+            // the first chunk >= from holding a peek / reset of the key (group flags first)
+            auto first_special = [&](uint32_t from) -> uint32_t {
+                for (uint32_t G = from / 64; G < f.n_groups;) {
+                    gwin(G);
+                    const uint32_t g = gwb + lane;
+                    const uint64_t m = __ballot(g >= G && g < f.n_groups && (g_w2 & 0xFFu));
+                    if (!m) { G = gwb + 64; continue; }
+                    const uint32_t gs = gwb + (uint32_t)__builtin_ctzll(m);
+                    const uint32_t c = gs * 64 + lane;
+                    const uint64_t* sm = summ_at(c < f.n_chunks ? c : 0u) + ow;
+                    const uint32_t w2 = c < f.n_chunks ? (uint32_t)sm[2] : 0u;
+                    const uint64_t mm = __ballot(c >= from && (w2 & 0xFFu));
+                    if (mm) return gs * 64 + (uint32_t)__builtin_ctzll(mm);
+                    G = gs + 1;
+                }
+                return kNone;
+            };
+            auto allowed1 = [&](int64_t t) { return hot_pred_k<A>(L, t, sa, sb, sc, 1); };
+            uint32_t cc = 0;                                  // cursor: chunks before it are decided
+            uint64_t ka = sa, kb = sb, kc = sc;               // the state at cc's start
+            uint32_t pc = 0, pofs = 0;                        // cc's walked allows: count, offsets
+            int64_t ts = lo;                                  // the next allow is at ms >= ts
+            bool must = false;                                // cc must be detailed (see detail_at)
+            int64_t W = 0;                                    // SW: the window of the thresholds in use
+            if constexpr (A == kAlgoSW) {
+                int64_t rr;
+                W = uni(jdiv(ts, L.window_ms, L.inv_window, &rr) * L.window_ms);
+            }
+            // A bound no correct walk reaches (every step moves the cursor chunk or ts forward):
+            // past it the walk stops and flags the batch (RL_E_CAPACITY) instead of spinning.
+            uint32_t guard = 4u * (span + f.n_chunks) + 4096u;
+            auto spin = [&]() {
+                if (guard != 0) --guard;
+                return guard == 0;
+            };
+            // a chunk detailed from the current state (the group walk's path), then the cursor past it
+            auto detail_at = [&](uint32_t c) {
+                T0 = hot_t0<A>(lo, hi, sa, sb, sc);
+                if (!t1_table(T0, T1)) T1 = t1_of(T0);
+                detail(c, INT64_MAX, INT64_MIN, 1u, 0ULL);
+                sa = uni(sa); sb = uni(sb); sc = uni(sc);
+                uint32_t w2;
+                int64_t mxc;
+                cinfo(c, w2, mxc);
+                cc = c + 1; ka = sa; kb = sb; kc = sc; pc = 0; pofs = 0;
+                // the next chunk's acquires in the last ms of this one come after every table
+                // entry of that ms in this chunk: if the state still grants there, detail it too
+                if (mxc != INT64_MIN) {
+                    if (mxc + 1 > ts) ts = mxc + 1;
+                    must = uni((uint32_t)allowed1(mxc)) != 0u;
+                }
+            };
+            // back to the cursor chunk's start state, to detail it (the detail counts its
+            // walked allows again)
+            auto undo_cursor = [&]() {
+                if (lane == 0) n_allowed -= pc;
+                sa = ka; sb = kb; sc = kc;
+            };
+            // (every chunk to detail goes through one call site: `detail` is inlined, and a
+            // copy per call site made the kernel's code several times larger)
+            uint32_t dc = kNone;
+            uint32_t spn = first_special(1);                  // the next special after the cursor
+            const uint64_t c_w0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+            for (;;) {
+                // (the loop-carried scalars re-declared uniform: a value the compiler cannot
+                // prove uniform turns every branch on it into an exec-mask region)
+                dc = uni(dc); cc = uni(cc); pc = uni(pc); pofs = uni(pofs); ts = uni(ts);
+                wb = uni(wb); guard = uni(guard); spn = uni(spn); cb = uni(cb); nb = uni(nb);
+                gwb = uni(gwb); must = uni((uint32_t)must) != 0u;
+                ka = uni(ka); kb = uni(kb); kc = uni(kc); sa = uni(sa); sb = uni(sb); sc = uni(sc);
+                if constexpr (A == kAlgoSW) W = uni(W);
+                if (dc != kNone) { detail_at(dc); dc = kNone; }
+                if (cc >= f.n_chunks || spin()) break;
+                if (spn <= cc) spn = first_special(cc + 1);   // (kNone is above every chunk)
+                // the cursor chunk: detailed when it must be or holds a special
+                if (pc == 0) {
+                    uint32_t w2;
+                    int64_t mxc;
+                    cinfo(cc, w2, mxc);
+                    if (must || (w2 & 0xFFu)) { must = false; dc = cc; continue; }
+                }
+                // the next allow: the first ms >= ts with an acquire the state grants; q1: the
+                // first ms >= ts the state grants anything at
+                int64_t tf = INT64_MIN, q1 = INT64_MAX;
+                uint32_t rf = 0, pf = 1;
+                const uint64_t c_f0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                for (;;) {
+                    ++n_find;
+                    ts = uni(ts); wb = uni(wb); guard = uni(guard); q1 = uni(q1);
+                    if (ts > hi || spin()) break;
+                    if (ts >= wb + 192) {                         // far ahead: refill the window
+                        wb = lo + ((ts - lo) & ~(int64_t)63);
+                        tA = tab(wb + lane); tB = tab(wb + 64 + lane); tC = tab(wb + 128 + lane);
+                    }
+                    while (ts >= wb + 64) {
+                        wb += 64; tA = tB; tB = tC; tC = tab(wb + 128 + lane);
+                    }
+                    int64_t lim_t = hi;                           // SW: the window's end - 1
+                    int64_t Q1 = 0, Q2 = 0;                       // SW: the window's thresholds
+                    if constexpr (A == kAlgoSW) {
+                        const int64_t w = L.window_ms;
+                        if (!(ts >= W && ts - W < w)) {
+                            int64_t rr;
+                            W = uni(jdiv(ts, w, L.inv_window, &rr) * w);
+                        }
+                        const SW2 s0 = sw_unpack(sa, sb, sc);
+                        const int64_t C = s0.b1_start == W ? (int64_t)s0.b1_cnt : 0;
+                        if (thr_w != W || C < thr_c || C - thr_c > 63) { thr_build(W, C); ++n_tk; }
+                        Q1 = (int64_t)readlane64((uint64_t)thr1, (uint32_t)(C - thr_c));
+                        Q2 = (int64_t)readlane64((uint64_t)thr2, (uint32_t)(C - thr_c));
+                        if (W + w - 1 < lim_t) lim_t = W + w - 1;
+                    }
+                    // one 64-ms view: what the state grants per ms (q), the first candidate
+                    auto view = [&](int64_t tb, const uint2 e) -> bool {
+                        const int64_t t = tb + (int64_t)lane;
+                        uint32_t q;
+                        if constexpr (A == kAlgoTB) {
+                            // tb_refill per lane, its elapsed time as (tb - last) + lane (exact:
+                            // integers below 2^53), no contraction (Lua :56-58)
+                            const int64_t last = (int64_t)sb;
+                            const double el = (double)(tb - last) + (double)lane;
+                            const double x = __longlong_as_double((long long)sa) + el * L.rate_per_ms;
+                            double bal = x < L.capacity ? x : L.capacity;
+                            if (!(sc & 1u) || t > last + L.ttl_ms) bal = L.capacity;
+                            q = bal >= 2.0 ? 2u : bal >= 1.0 ? 1u : 0u;
+                        } else {
+                            q = t >= Q2 ? 2u : t >= Q1 ? 1u : 0u;
+                        }
+                        if (!(t >= ts && t <= lim_t)) q = 0;
+                        const uint64_t mq = __ballot(q != 0);
+                        if (mq && q1 == INT64_MAX) q1 = tb + (int64_t)__builtin_ctzll(mq);
+                        const uint32_t cnd = q >= 2u ? e.y : q == 1u ? e.x : kWalkNone;
+                        const uint64_t m = __ballot(cnd != kWalkNone);
+                        if (!m) return false;
+                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                        rf = (uint32_t)__builtin_amdgcn_readlane((int)cnd, (int)l);
+                        const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)e.x, (int)l);
+                        pf = rf != ex ? 2u : 1u;                  // (q >= 2 and a 2-permit acquire first)
+                        tf = tb + (int64_t)l;
+                        return true;
+                    };
+                    if (view(wb, tA) || view(wb + 64, tB)) break;
+                    ts = lim_t < wb + 127 ? lim_t + 1 : wb + 128;  // (SW: the next window)
+                }
+                if (a.dbg) cyc_find += __builtin_amdgcn_s_memtime() - c_f0;
+                // (no allow before the batch ends: the rest is denied, up to the next special)
+                const uint32_t cs = tf == INT64_MIN ? f.n_chunks - 1u : rf / kHotChunk;
+                const uint32_t cfl = 13u | ((pc - 1u) << 4) | (pofs << 8);   // cc's verdict, pc > 0
+                const uint64_t c_c0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                if (spn <= cs || tf == INT64_MIN) {               // a special in (cc, cs] / the end
+                    enter(cc & ~63u);
+                    const uint32_t fl = pc ? cfl : deny_fl(q1);
+                    if (cb + lane == cc) { vA = ka; vB = kb; vC = kc; vF = fl; }
+                    const uint32_t e = spn <= cs ? spn : f.n_chunks;
+                    deny(cc + 1, e, sa, sb, sc, q1);
+                    if (e == f.n_chunks) break;
+                    dc = spn;
+                    continue;
+                }
+                if (cs == cc && pc > 0) {                         // another allow in the cursor chunk
+                    if (pc == 4) { undo_cursor(); dc = cc; continue; }
+                } else if (cs > cc) {
+                    const uint32_t fl = pc ? cfl : deny_fl(q1);
+                    if (cc >= cb && cs < cb + 64) {               // (the common case: one block)
+                        const uint32_t c = cb + lane;
+                        const uint32_t dfl = deny_fl(q1);
+                        if (c == cc) { vA = ka; vB = kb; vC = kc; vF = fl; }
+                        else if (c > cc && c < cs) { vA = sa; vB = sb; vC = sc; vF = dfl; }
+                    } else {
+                        enter(cc & ~63u);
+                        const uint32_t fl2 = pc ? cfl : deny_fl(q1);
+                        if (cb + lane == cc) { vA = ka; vB = kb; vC = kc; vF = fl2; }
+                        deny(cc + 1, cs, sa, sb, sc, q1);
+                    }
+                    cc = cs; ka = sa; kb = sb; kc = sc; pc = 0; pofs = 0;
+                }
+                const uint64_t c_a0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                if (a.dbg) cyc_close += c_a0 - c_c0;
+                pofs |= (rf % kHotChunk) << (6 * pc);
+                ++pc;
+                // the allow (Lua :61-64 / SlidingWindowRateLimiter :114-116) at ms tf
+                bool burst;
+                if constexpr (A == kAlgoTB) {
+                    const double nt = uni(tb_refill(L, tf, sa, sb, sc) - (double)pf);
+                    sa = (uint64_t)__double_as_longlong(nt);
+                    sb = (uint64_t)tf;
+                    sc = 1;
+                    burst = nt >= 1.0;                            // (elapsed 0: the balance is nt)
+                } else {
+                    SWGeo gl{};
+                    gl.curr_start = W;
+                    sw_commit_allows(L, gl, sa, sb, sc, 1u, tf);
+                    sa = uni(sa); sb = uni(sb); sc = uni(sc);
+                    // the window's table at the new count, when it holds it
+                    const int64_t C = (int64_t)sw_unpack(sa, sb, sc).b1_cnt;
+                    if (thr_w == W && C >= thr_c && C - thr_c <= 63)
+                        burst = tf >= (int64_t)readlane64((uint64_t)thr1, (uint32_t)(C - thr_c));
+                    else
+                        burst = allowed1(tf);
+                }
+                if (lane == 0) ++n_allowed;
+                ++n_changed;
+                ++n_walk;
+                ts = tf + 1;
+                if (burst) {                                      // the next request of ms tf too: detail
+                    undo_cursor();
+                    dc = cc;
+                }
+                if (a.dbg) cyc_allow += __builtin_amdgcn_s_memtime() - c_a0;
+            }
+            flush();
+            if (guard == 0 && lane == 0) atomicAdd(&a.ctl->cap_err, 1ULL);
+            if (a.dbg) cyc_walk += __builtin_amdgcn_s_memtime() - c_w0;
+            wave_fence();
+            if (lane == 0) { S.sa[hs] = sa; S.sb[hs] = sb; S.sc[hs] = sc; }
+            wave_fence();
+            return true;
+        };
+        if (walk()) {
+            if (a.dbg) cyc_pass1 += __builtin_amdgcn_s_memtime() - c_p1;
+            return;
+        }
         // level 2: 64 groups per test, the next 64 in flight
         ulonglong2 nx01 = *(const ulonglong2*)(grp_at(lane) + ow);
         uint64_t nx2 = grp_at(lane)[ow + 2], nx3 = grp_at(lane)[ow + 3];
@@ -1072,6 +1515,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             d[8] = cyc_pre; d[9] = cyc_pass1; d[10] = cyc_pass2; d[11] = n_other; d[12] = n_prehit;
             d[13] = cyc_build; d[14] = n_bisect;
             d[15] = cyc_sw[0]; d[16] = cyc_sw[1]; d[17] = cyc_sw[2]; d[18] = cyc_sw[3]; d[19] = n_sw_it;
+            d[20] = n_walk; d[21] = n_find; d[22] = cyc_find; d[23] = cyc_walk;
+            d[24] = cyc_close; d[25] = cyc_allow; d[26] = n_enter;
         }
     }
 }
@@ -1079,18 +1524,65 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 // The hot chains alone (single-wave workgroups), launched on a side stream of the device's
 // highest priority just before the normal regions' launch, so they start first. They are a
 // few hundred lone waves beside ~10^6 normal-region waves: a larger register budget costs
-// no occupancy that matters.
-#ifndef RL_CHAIN_MIN_WAVES
-#define RL_CHAIN_MIN_WAVES 2
-#endif
+// no occupancy that matters: one wave per SIMD gives the walk's registers room (512 VGPRs,
+// no spills).
+constexpr int kChainMinWaves = 1;
 template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(64, RL_CHAIN_MIN_WAVES) void k_hot_chains(RegionArgs a) {
+__global__ __launch_bounds__(64, kChainMinWaves) void k_hot_chains(RegionArgs a) {
     __shared__ RegionLds<Codec, true> S;
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     for (uint32_t i = blockIdx.x; i < hc; i += gridDim.x) {       // (workgroup-uniform)
         wave_fence();                                             // the last chain's LDS users
         hot_chain<Codec, Res, TOK>(a, i, S);
     }
+}
+
+// A chunk a chain's allow walk decided (verdict bit 2): the key's records under the state in
+// sm[0..2], but the allowed ones (bit 3: bits 4-5 hold their count - 1, bits 16-39 their
+// offsets, 6 bits each, ascending) and, after each, the state that allow leaves (TB: Lua
+// :56-64; SW: the INCR of :114-116). Every lane runs it (the allowed records' times and
+// permits are read from their lanes); `mine`: this lane holds the key's record.
+template <class Res, bool TOK>
+__device__ inline void walk_fill_key(const RegionArgs& a, const DevLimiter& L, const uint64_t* sm,
+                                     uint64_t v, const Req& q, bool mine, uint32_t lane, uint32_t j) {
+    const bool tb = L.algo == kAlgoTB;
+    uint64_t ya = sm[0], yb = sm[1], yc = sm[2];        // the state after the allows so far
+    uint64_t sa = ya, sb = yb, sc = yc;                  // this lane's: after the last allow before it
+    bool at = false;
+    double nt = 0.0, nt_at = 0.0;
+    const uint32_t na = (v & 8u) ? (uint32_t)((v >> 4) & 3u) + 1u : 0u;
+    for (uint32_t k = 0; k < na; ++k) {
+        const uint32_t o = (uint32_t)(v >> (16 + 6 * k)) & 63u;
+        const int64_t t_o = (int64_t)readlane64((uint64_t)q.now_ms, o);
+        const int32_t p_o = __builtin_amdgcn_readlane(q.permits, (int)o);
+        if (tb) {
+            nt = tb_refill(L, t_o, ya, yb, yc) - (double)p_o;
+            ya = (uint64_t)__double_as_longlong(nt); yb = (uint64_t)t_o; yc = 1;
+        } else {
+            sw_commit_allows(L, sw_geo(t_o, L), ya, yb, yc, 1u, t_o);
+        }
+        if (lane == o) { at = true; nt_at = nt; }
+        if (lane >= o) { sa = ya; sb = yb; sc = yc; }
+    }
+    if (!mine) return;
+    bool alw = false;
+    int64_t rem;
+    double tk = __builtin_nan("");
+    if (tb && (int64_t)q.permits > L.max_permits) {
+        rem = kRemUnknown;                                  // :110-116
+    } else {
+        alw = at;
+        if (tb) {
+            tk = at ? nt_at : tb_refill(L, q.now_ms, sa, sb, sc);
+            rem = d2l(tk);
+        } else {
+            const int64_t r = L.max_permits - sw_estimate(sw_unpack(sa, sb, sc), sw_geo(q.now_ms, L),
+                                                          q.now_ms, L.window_ms);
+            rem = r > 0 ? r : 0;
+        }
+    }
+    put_res<Res>(a, j, alw, rem);
+    if (TOK) a.tok[j] = tk;
 }
 
 // Phase C (one wave per group of 64 chunks, all CUs): results of the chunks the chains
@@ -1128,6 +1620,25 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
             const uint64_t v0 = (g0 & 1u) ? ((g0 & 3u) | (c0w & 0xFF00u)) : c0w;
             const uint64_t v1 = (g1 & 1u) ? (g1 & 3u) : c1w;
             const uint32_t j = f.start + c * kHotChunk + lane;
+            if ((v0 | v1) & 4u) {                        // an allow walk's verdict (chunk level)
+                const bool valid = j < f.end;
+                const Req q = Codec::dec(recs[valid ? j : f.start], base);
+                const uint64_t* s1 = a.hot_summ + (size_t)(f.chunk_base + c) * 8;
+                const bool ok = valid && !q.invalid;
+                if (v0 & 4u) walk_fill_key<Res, TOK>(a, L, s1, v0, q, ok && q.h == f.tag, lane, j);
+                if (v1 & 4u) walk_fill_key<Res, TOK>(a, L, s1 + 4, v1, q, ok && q.h == f.tag2, lane, j);
+                // (a key with a plain verdict beside a walked one: as below)
+                if (((v0 & 5u) == 1u && q.h == f.tag) || ((v1 & 5u) == 1u && q.h == f.tag2)) {
+                    if (ok) {
+                        const uint64_t* sm = (q.h == f.tag ? ((g0 & 1u) ? s2 : s1) : ((g1 & 1u) ? s2 : s1) + 4);
+                        const bool early = L.algo == kAlgoTB && (int64_t)q.permits > L.max_permits;
+                        res[j] = (Res)pack_result(false, early ? kRemUnknown : 0);
+                        if (TOK) a.tok[j] = (L.algo == kAlgoTB && !early) ? tb_refill(L, q.now_ms, sm[0], sm[1], sm[2])
+                                                                         : __builtin_nan("");
+                    }
+                }
+                continue;
+            }
             if (j >= f.end) continue;
             // the decided keys' records here are acquires (n_special == 0); TB permits > max
             // (verdict bit 1) are the only ones not (deny, 0); other records are the chains'

@@ -107,11 +107,8 @@ __device__ inline int64_t batch_hi(const BatchCtl* c) {
 // unpermute's position reads and output writes. They keep L2 / Infinity Cache for the
 // scattered record runs, the state table and the packed results the unpermute gathers
 // (tb_uniform 3.33 -> 3.12 ms/step on MI355X). Scattered record stores stay temporal: a
-// streaming partial-line store goes to memory on its own (scatter 1.5 -> 3.3 ms).
-// A/B builds: -DRL_TEMPORAL=1 turns the streaming accesses off, -DRL_NT_SCATTER_REC on.
-#ifndef RL_TEMPORAL
-#define RL_TEMPORAL 0
-#endif
+// streaming partial-line store goes to memory on its own (scatter 1.5 -> 3.3 ms); the
+// upsweep's key reads too (streaming them measured no faster, rounds 3-4).
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 template <bool NT, class T>
 __device__ inline T ld(const T* p) {
@@ -133,18 +130,10 @@ __device__ inline void st_rec(Rec* p, const Rec& r) {
         *p = r;
     }
 }
-constexpr bool kNtScIn = !RL_TEMPORAL;
-#ifdef RL_NT_SCATTER_REC
-constexpr bool kNtScRec = true;
-#else
+constexpr bool kNtScIn = true;
 constexpr bool kNtScRec = false;
-#endif
-constexpr bool kNtScPos = !RL_TEMPORAL;
-#ifdef RL_NT_UPSWEEP
-constexpr bool kNtUp = true;
-#else
+constexpr bool kNtScPos = true;
 constexpr bool kNtUp = false;
-#endif
 template <bool NT, class Rec>
 __device__ inline Rec ld_rec(const Rec* p) {
     if constexpr (NT && sizeof(Rec) == 16) {
@@ -156,8 +145,8 @@ __device__ inline Rec ld_rec(const Rec* p) {
         return *p;
     }
 }
-constexpr bool kNtRgRec = !RL_TEMPORAL;
-constexpr bool kNtUn = !RL_TEMPORAL;
+constexpr bool kNtRgRec = true;
+constexpr bool kNtUn = true;
 
 template <int NT>
 __device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_tmp /*[NT/64]*/,
@@ -195,21 +184,11 @@ __device__ inline void load_lim_lds(LimLds& L, const PartArgs& a) {
 }
 
 // Tile processed by this workgroup at iteration `it` of a persistent grid: the
-// workgroups of one XCD (blocks b, b+8, ...) take consecutive tiles.
-// RL_TILE_ORDER 1 (A/B knob): XCD x instead owns the contiguous chunk [x*T/8, (x+1)*T/8) and
-// its workgroups walk it 32 tiles at a time, so a bin's record run is split between XCDs 8 times
-// in total rather than once per 256 tiles. Returns >= n_tiles when this workgroup is done.
-#ifndef RL_TILE_ORDER
-#define RL_TILE_ORDER 0
-#endif
+// workgroups of one XCD (blocks b, b+8, ...) take consecutive tiles. (Giving each XCD one
+// contiguous eighth of the tiles instead measured no faster, round 4.) Returns >= n_tiles when
+// this workgroup is done.
 __device__ inline uint32_t tile_at(uint32_t it, uint32_t n_tiles) {
-    if constexpr (RL_TILE_ORDER == 1) {
-        if (gridDim.x % 8 == 0) {
-            const uint32_t per = gridDim.x / 8, chunk = (n_tiles + 7) / 8;
-            const uint32_t k = it * per + blockIdx.x / 8;
-            return k < chunk ? (blockIdx.x % 8) * chunk + k : n_tiles;
-        }
-    }
+    (void)n_tiles;
     return it * gridDim.x + xcd_remap(blockIdx.x, gridDim.x);
 }
 

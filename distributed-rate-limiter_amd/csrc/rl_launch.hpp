@@ -138,8 +138,13 @@ struct RegionArgs {
     const uint32_t* route_list;
     const uint32_t* route_start;
     const uint32_t* route_cnt;
+    // Allow walks (nullable): per key of the first walk_regions() listed regions
+    // (slot 2 * i + key), per ms of the batch's span, the first record (relative to the
+    // region's start) of the key's plain acquires of 1 permit (.x) and of at most 2 (.y) in
+    // that ms; kWalkNone = none. Built by k_hot_summ, read by the chains (hot_chain, walk).
+    uint2* walk_tab;
+    uint32_t walk_min;         // walked keys expect at least this many allows (walk_dense)
 };
-
 constexpr int kMaxShards = 64;              // routing: shards per router
 // Hot-key owner directory (rl_set_owner_directory): at most kDirMax keys in kDirSlots slots.
 constexpr uint32_t kDirSlots = 8192;
@@ -147,6 +152,25 @@ constexpr uint32_t kDirMax = 4096;
 constexpr uint32_t kDirEmpty = 0xFFFFFFFFu;
 struct DirSlot { uint64_t tag; uint32_t owner; uint32_t pad; };
 constexpr uint32_t kHotMax = 1024;       // hot regions per batch (<= one k_hot_scan block)
+// Allow walks: one table per key of the listed hot regions (slot 2 i + key), each over the
+// batch's time span (at most kWalkSpan ms) rounded up to 64 entries: 512 MiB hold 256 regions'
+// tables at the longest span, all 1024 at a span up to 32 s.
+constexpr uint32_t kWalkSpan = 1u << 17;
+constexpr uint32_t kWalkNone = 0xFFFFFFFFu;
+// A chain's allows are a dependent sequence (~4K cycles each on the chunk path): below a few
+// thousand of them the chain ends before the normal regions drain and a walk only adds its
+// table build and verdict fills (sw_zipf: 1000/min keys, ~1-3K allows, +0.3 ms/step walked).
+constexpr uint32_t kWalkMinAllows = 4000;
+constexpr size_t kWalkTabEntries = (size_t)1 << 26;
+__host__ __device__ inline uint32_t walk_stride(int64_t lo, int64_t hi) {
+    return (uint32_t)((hi - lo + 64) & ~(int64_t)63);
+}
+// listed regions with tables (the first ones of the hot list)
+__host__ __device__ inline uint32_t walk_regions(int64_t lo, int64_t hi) {
+    if (hi < lo || (uint64_t)(hi - lo) >= kWalkSpan) return 0;
+    const size_t r = kWalkTabEntries / (2 * (size_t)walk_stride(lo, hi));
+    return r < kHotMax ? (uint32_t)r : kHotMax;
+}
 // hot_list layout: [kHotMax] list, then the selection's meta words: [0] listed count,
 // [1 .. 33] size-class histogram, [kHotClassCursor ..+33] per-class list cursors, then
 // [kHotTotalOff .. +2] chunk / group totals (k_hot_scan), [kHotRoutedOff] routed entries
@@ -168,7 +192,7 @@ __host__ __device__ inline void route_slots(uint32_t region, uint32_t& s1, uint3
     s2 = ((region ^ 0x5BD1E995u) * 0x85EBCA6Bu) >> 21;
 }
 constexpr uint32_t kHotChunk = 64;       // records per summary chunk (one wave)
-constexpr uint32_t kDbgWords = 24;       // debug words per bin
+constexpr uint32_t kDbgWords = 28;       // debug words per bin
 // Batch counters are sharded: one device-scope atomic word sustains only ~88 adds per us
 // (MI355X_MICROARCH.md, rows 'dequeue' / 'fanin'), and every region wave adds to them, so a
 // 1.3M-region batch on ONE set of words serialises for >10 ms. Region waves add to slot

@@ -160,10 +160,7 @@ __device__ inline void scatter_outputs(const PartArgs& a, Rec*& out_norm, int64_
     lo_route = a.route_list ? a.lo_bins : 0xFFFFFFFFu;
 }
 
-#ifndef RL_SCATTER_DEPTH
-#define RL_SCATTER_DEPTH 8
-#endif
-constexpr int kScatterDepth = RL_SCATTER_DEPTH;   // rounds of inputs in flight (divides kTileItems)
+constexpr int kScatterDepth = 8;   // rounds of inputs in flight (divides kTileItems)
 
 template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
@@ -317,10 +314,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
 // encode each round and stage its records and digits in LDS one round ahead; the ranking
 // waves (threads 0..kTileThreads-1) read them from LDS, rank, and store — they issue no
 // global load inside a tile, so nothing ever waits behind their stores.
-#ifndef RL_SPLIT_DEPTH
-#define RL_SPLIT_DEPTH 4
-#endif
-constexpr int kSplitDepth = RL_SPLIT_DEPTH;       // loader rounds in flight (divides kTileItems)
+constexpr int kSplitDepth = 4;       // loader rounds in flight (divides kTileItems)
 template <class Codec>
 __host__ __device__ inline size_t split_stage_off(uint32_t bins) {     // in u64 words, 16-B aligned
     return ((size_t)bins + (bins + 1) / 2 + 1) & ~(size_t)1;

@@ -41,10 +41,7 @@ struct RegionLds : RegionTable {
 template <class Codec>
 struct RegionLds<Codec, false> : RegionTable {};
 
-#ifndef RL_NO_SPARSE
-#define RL_NO_SPARSE 0                    // A/B builds: 1 compiles the sparse-region path out
-#endif
-constexpr bool kSparseOn = !RL_NO_SPARSE;
+constexpr bool kSparseOn = true;                 // (rl_tune ablate kAblNoProbe turns it off at run time)
 
 // Sparse region (few records): the LDS table starts with every bucket kOccUnloaded and a
 // probe that reaches such a bucket faults it in from HBM (128 B, + 32 B of cache words);
@@ -745,12 +742,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     }
 }
 
-#ifndef RL_HOT_MIN_WAVES
-#define RL_HOT_MIN_WAVES 4
-#endif
-// Normal regions (one wave each) at >= RL_REGION_MIN_WAVES waves per SIMD (VGPR budget).
-#ifndef RL_REGION_MIN_WAVES
-#define RL_REGION_MIN_WAVES 4
-#endif
+// Normal regions (one wave each) at >= kRegionMinWaves waves per SIMD (VGPR budget).
+constexpr int kRegionMinWaves = 4;
 
 }  // namespace rl

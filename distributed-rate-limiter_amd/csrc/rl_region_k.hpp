@@ -8,7 +8,7 @@
 namespace rl {
 
 template <class Codec, class Res, bool TOK, bool CACHE = false>
-__global__ __launch_bounds__(64, CACHE ? 3 : RL_REGION_MIN_WAVES) void k_regions(RegionArgs a) {
+__global__ __launch_bounds__(64, CACHE ? 3 : kRegionMinWaves) void k_regions(RegionArgs a) {
     if constexpr (CACHE) {                       // some limiter keeps a local cache
         __shared__ RegionTableX S;
         region_body_t<Codec, Res, TOK>(a, blockIdx.x, S);

@@ -391,7 +391,7 @@ class Engine:
 
     def debug_region_times(self, n_bins):
         """Per-bin {t_start, t_end, records, rounds} of the last batch (rl_tune debug_regions)."""
-        out = np.zeros((n_bins, 24), np.uint64)     # kDbgWords
+        out = np.zeros((n_bins, 28), np.uint64)     # kDbgWords
         k = self._L.rl_debug_fetch(self._h, b"region_times", _p(out), out.nbytes)
         if k < 0:
             raise RlError(k, "rl_debug_fetch")

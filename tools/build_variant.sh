@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B build of librl_engine.so with extra -D flags into distributed-rate-limiter_amd/variants/<name>/ (run here, on CPU).
-# usage: tools/build_variant.sh <name> "-DRL_TILE_ITEMS=64 ..." [git-rev]
+# usage: tools/build_variant.sh <name> "<extra hipcc flags>" [git-rev]   (A/B: a revision with the constant changed)
 #   git-rev: build that revision's sources (e.g. HEAD, the A/B base) instead of the working tree
 set -e
 root="$(cd "$(dirname "$0")/.." && pwd)"

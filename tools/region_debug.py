@@ -73,7 +73,10 @@ for b in range(args.batches):
                 f"T1 updates {(rr >> 32) & 0xFFFF:6d} HOT Mcyc det/run/T1 {cyc} pre/pass1/pass2 {cyc2} "
                 f"other-key recs {int(d[i, 11])} prefetched {int(d[i, 12])} build Mcyc {d[i, 13] / 1e6:.2f} "
                 f"bisect lanes {int(d[i, 14])} SW run Mcyc setup/greedy/rem/commit "
-                f"{' '.join(f'{x / 1e6:.2f}' for x in d[i, 15:19])} greedy steps {int(d[i, 19])}"
+                f"{' '.join(f'{x / 1e6:.2f}' for x in d[i, 15:19])} greedy steps {int(d[i, 19])} "
+                f"WALK allows {int(d[i, 20])} finds {int(d[i, 21])} Mcyc find/walk "
+                f"{d[i, 22] / 1e6:.2f} {d[i, 23] / 1e6:.2f} close/allow {d[i, 24] / 1e6:.2f} "
+                f"{d[i, 25] / 1e6:.2f} block loads {int(d[i, 26])}"
                 if hot[i] else f"rounds {rr:8d}")
         print(f"   dur {dur[i]:9.1f} us start {(d[i, 0] - t0) / 100:9.1f} us  lim {lim_of[i]} "
               f"recs {int(d[i, 2]):9d} {what}")
