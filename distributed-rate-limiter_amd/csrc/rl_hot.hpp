@@ -1551,6 +1551,7 @@ __device__ inline void walk_fill_key(const RegionArgs& a, const DevLimiter& L, c
     bool at = false;
     double nt = 0.0, nt_at = 0.0;
     const uint32_t na = (v & 8u) ? (uint32_t)((v >> 4) & 3u) + 1u : 0u;
+#pragma unroll 1
     for (uint32_t k = 0; k < na; ++k) {
         const uint32_t o = (uint32_t)(v >> (16 + 6 * k)) & 63u;
         const int64_t t_o = (int64_t)readlane64((uint64_t)q.now_ms, o);
@@ -1588,7 +1589,10 @@ __device__ inline void walk_fill_key(const RegionArgs& a, const DevLimiter& L, c
 // Phase C (one wave per group of 64 chunks, all CUs): results of the chunks the chains
 // decided. The group's chunk verdicts come in with one load per lane; a chunk holding only
 // the dominant key's records is written without reading them (unless TB balances are out).
-template <class Codec, class Res, bool TOK>
+// WALK: the chunks of allow walks' verdicts only (bit 2), which the other instance skips —
+// their exact per-record arithmetic would otherwise set the register budget of every fill
+// wave (80 VGPRs instead of 38).
+template <class Codec, class Res, bool TOK, bool WALK>
 __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
     __shared__ uint32_t s_base[kHotMax + 1];
     const uint32_t hc = min(a.hot_count[0], kHotMax);
@@ -1609,7 +1613,8 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
         // lane l: chunk c0 + l's verdict words of both keys
         const uint64_t* s1l = a.hot_summ + (size_t)(f.chunk_base + min(c0 + lane, c1 - 1)) * 8;
         const uint64_t cv0 = s1l[3], cv1 = s1l[7];
-        const uint64_t any = __ballot(c0 + lane < c1 && (((g0 | cv0) & 1u) || ((g1 | cv1) & 1u)));
+        const uint64_t any = WALK ? __ballot(c0 + lane < c1 && ((((g0 & 1u) ? 0u : cv0) | ((g1 & 1u) ? 0u : cv1)) & 4u))
+                                  : __ballot(c0 + lane < c1 && (((g0 | cv0) & 1u) || ((g1 | cv1) & 1u)));
         if (!any) continue;
         const DevLimiter& L = a.lims[a.region_lim[f.bin]];
         for (uint64_t m = any; m; m &= m - 1) {
@@ -1621,6 +1626,7 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
             const uint64_t v1 = (g1 & 1u) ? (g1 & 3u) : c1w;
             const uint32_t j = f.start + c * kHotChunk + lane;
             if ((v0 | v1) & 4u) {                        // an allow walk's verdict (chunk level)
+                if constexpr (!WALK) continue;
                 const bool valid = j < f.end;
                 const Req q = Codec::dec(recs[valid ? j : f.start], base);
                 const uint64_t* s1 = a.hot_summ + (size_t)(f.chunk_base + c) * 8;
@@ -1639,6 +1645,7 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
                 }
                 continue;
             }
+            if constexpr (WALK) continue;
             if (j >= f.end) continue;
             // the decided keys' records here are acquires (n_special == 0); TB permits > max
             // (verdict bit 1) are the only ones not (deny, 0); other records are the chains'
@@ -1672,8 +1679,12 @@ hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs) {
 template <class Codec, class Res>
 hipError_t hot_fill_t(const RegionArgs& a, hipStream_t s) {
     const dim3 gp(persistent_grid(1u << 30, 4));
-    if (a.tok) hipLaunchKernelGGL((k_hot_fill<Codec, Res, true>), gp, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_hot_fill<Codec, Res, false>), gp, dim3(256), 0, s, a);
+    if (a.tok) hipLaunchKernelGGL((k_hot_fill<Codec, Res, true, false>), gp, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_hot_fill<Codec, Res, false, false>), gp, dim3(256), 0, s, a);
+    if (a.walk_tab) {                                 // (allow walks on: their verdicts)
+        if (a.tok) hipLaunchKernelGGL((k_hot_fill<Codec, Res, true, true>), gp, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_hot_fill<Codec, Res, false, true>), gp, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 
