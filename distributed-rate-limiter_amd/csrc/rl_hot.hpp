@@ -450,9 +450,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     if (i >= hc) return;
     // the passes are sequential critical paths beside thousands of normal-region waves
     __builtin_amdgcn_s_setprio(3);
-    const HotInfo f = uni(a.hot_info[i]);
+    const HotInfo f = a.hot_info[i];
     const uint32_t region = f.bin;                    // a bin is one region
-    const DevLimiter L = uni(a.lims[uni((uint32_t)a.region_lim[region])]);
+    const DevLimiter L = a.lims[a.region_lim[region]];
     const int64_t base = uni(a.ctl->base_ms);
     const int64_t lo = uni(batch_lo(a.ctl));
     const int64_t hi = uni(batch_hi(a.ctl));
