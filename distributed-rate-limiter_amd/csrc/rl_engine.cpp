@@ -779,6 +779,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ra.walk_tab = e->walk ? e->walk_tab : nullptr;
         ra.walk_min = e->walk_min;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
+        HIP_OK(launch_chains(ra, wide, res_bytes, s, e->hstream, e->hot_ev[0]));
     }
     if (e->region_order) {
         if (e->order_cap < n_bins) {
@@ -801,8 +802,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         HIP_OK(launch_solo(ra, wide, res_bytes, (uint32_t*)rstart, (uint32_t*)rcount, e->solo_list, cnt, s));
     }
     mark(e, 7);
-    // hot chains first (side stream), then the regions
-    HIP_OK(launch_region(ra, wide, res_bytes, s, e->hstream, e->hot_ev[0], e->hot_ev[1]));
+    // the regions (the hot chains run on the side stream since launch_chains)
+    HIP_OK(launch_region(ra, wide, res_bytes, s, hot ? e->hstream : nullptr, e->hot_ev[1]));
     mark(e, 10);
     if (hot) HIP_OK(launch_hot_fill(ra, wide, res_bytes, s));
     // the next batch's routed regions: this batch's largest hot regions (two-pass tables)

@@ -263,9 +263,13 @@ hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, con
           : res_bytes == 2 ? F<CodecC, uint16_t>(__VA_ARGS__)            \
                            : F<CodecC, uint32_t>(__VA_ARGS__))
 
+hipError_t launch_chains(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
+                         hipStream_t hs, hipEvent_t e0) {
+    return RL_BY_WIDTH(chains_launch_t, a, s, hs, e0);
+}
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
-                         hipStream_t hs, hipEvent_t e0, hipEvent_t e1) {
-    return RL_BY_WIDTH(region_launch_t, a, s, hs, e0, e1);
+                         hipStream_t hs, hipEvent_t e1) {
+    return RL_BY_WIDTH(region_launch_t, a, s, hs, e1);
 }
 hipError_t launch_hot_fill(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s) {
     return RL_BY_WIDTH(hot_fill_t, a, s);

@@ -308,12 +308,19 @@ hipError_t launch_scan_rows(const uint32_t* in, uint32_t* out, uint32_t rows, ui
 hipError_t launch_scan_small(const uint32_t* in, uint32_t* out, uint32_t len, hipStream_t s);
 hipError_t launch_add_rows(const uint32_t* row_base, uint32_t* data, uint32_t rows,
                            uint32_t cols, hipStream_t s);
-// hs (nullable): side stream for the hot chains (k_hot_chains), ordered by events e0 / e1.
+// The hot chains (k_hot_chains) on the side stream hs after event e0 on s, launched before
+// the region-order and solo kernels so that their single waves (one SIMD's registers each)
+// are dispatched ahead of the normal regions' ~10^6 waves; launch_region then runs the
+// normal regions on s and (hs non-null) joins hs by event e1.
+hipError_t launch_chains(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
+                         hipStream_t hs, hipEvent_t e0);
 hipError_t launch_region(const RegionArgs& a, bool wide, int res_bytes, hipStream_t s,
-                         hipStream_t hs = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                         hipStream_t hs = nullptr, hipEvent_t e1 = nullptr);
 // per record codec / packed result width (instantiated in csrc/rl_rt_*.hip)
 template <class Codec, class Res>
-hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0, hipEvent_t e1);
+hipError_t chains_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0);
+template <class Codec, class Res>
+hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e1);
 template <class Codec, class Res> hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs);
 template <class Codec, class Res> hipError_t hot_fill_t(const RegionArgs& a, hipStream_t s);
 hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStream_t s);

@@ -22,13 +22,16 @@ __global__ __launch_bounds__(64, CACHE ? 3 : kRegionMinWaves) void k_regions(Reg
 // from and joined to the engine stream by events) beside one single-wave workgroup per
 // normal region.
 template <class Codec, class Res>
-hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0,
-                           hipEvent_t e1) {
+hipError_t chains_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e0) {
+    (void)hipEventRecord(e0, s);
+    (void)hipStreamWaitEvent(hs, e0, 0);
+    (void)hot_chains_t<Codec, Res>(a, hs);
+    return hipGetLastError();
+}
+template <class Codec, class Res>
+hipError_t region_launch_t(const RegionArgs& a, hipStream_t s, hipStream_t hs, hipEvent_t e1) {
     const dim3 b(64), g(a.n_regions);
-    if (a.hot_mark && hs) {
-        (void)hipEventRecord(e0, s);
-        (void)hipStreamWaitEvent(hs, e0, 0);
-        (void)hot_chains_t<Codec, Res>(a, hs);
+    if (a.hot_mark && hs) {                          // (the chains are running on hs)
         // (a cache-on limiter beside hot ones: its regions run in the cache variant)
         if (a.cache && a.tok) hipLaunchKernelGGL((k_regions<Codec, Res, true, true>), g, b, 0, s, a);
         else if (a.cache) hipLaunchKernelGGL((k_regions<Codec, Res, false, true>), g, b, 0, s, a);

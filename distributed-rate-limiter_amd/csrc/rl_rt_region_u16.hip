@@ -2,6 +2,6 @@
 #include "rl_region_k.hpp"
 
 namespace rl {
-template hipError_t region_launch_t<CodecC, uint16_t>(const RegionArgs&, hipStream_t, hipStream_t,
-                                           hipEvent_t, hipEvent_t);
+template hipError_t chains_launch_t<CodecC, uint16_t>(const RegionArgs&, hipStream_t, hipStream_t, hipEvent_t);
+template hipError_t region_launch_t<CodecC, uint16_t>(const RegionArgs&, hipStream_t, hipStream_t, hipEvent_t);
 }  // namespace rl
