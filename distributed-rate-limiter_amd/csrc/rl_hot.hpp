@@ -1199,134 +1199,144 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                     cinfo(cc, w2, mxc);
                     if (must || (w2 & 0xFFu)) { must = false; dc = cc; continue; }
                 }
-                // the next allow: the first ms >= ts with an acquire the state grants; q1: the
-                // first ms >= ts the state grants anything at
-                int64_t tf = INT64_MIN, q1 = INT64_MAX;
-                uint32_t rf = 0, pf = 1;
-                const uint64_t c_f0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                // The common path as a loop of its own (find, verdicts, allow: the cursor chunk
+                // always holds a walked allow here), so that the register allocator weighs the
+                // values it uses above the rest of the chain's; anything else leaves it.
+                bool done = false;
                 for (;;) {
-                    ++n_find;
-                    ts = uni(ts); wb = uni(wb); guard = uni(guard); q1 = uni(q1);
-                    if (ts > hi || spin()) break;
-                    if (ts >= wb + 192) {                         // far ahead: refill the window
-                        wb = lo + ((ts - lo) & ~(int64_t)63);
-                        tA = tab(wb + lane); tB = tab(wb + 64 + lane); tC = tab(wb + 128 + lane);
-                    }
-                    while (ts >= wb + 64) {
-                        wb += 64; tA = tB; tB = tC; tC = tab(wb + 128 + lane);
-                    }
-                    int64_t lim_t = hi;                           // SW: the window's end - 1
-                    int64_t Q1 = 0, Q2 = 0;                       // SW: the window's thresholds
-                    if constexpr (A == kAlgoSW) {
-                        const int64_t w = L.window_ms;
-                        if (!(ts >= W && ts - W < w)) {
-                            int64_t rr;
-                            W = uni(jdiv(ts, w, L.inv_window, &rr) * w);
+                    cc = uni(cc); pc = uni(pc); pofs = uni(pofs); ts = uni(ts); cb = uni(cb);
+                    ka = uni(ka); kb = uni(kb); kc = uni(kc); sa = uni(sa); sb = uni(sb); sc = uni(sc);
+                    // the next allow: the first ms >= ts with an acquire the state grants; q1: the
+                    // first ms >= ts the state grants anything at
+                    int64_t tf = INT64_MIN, q1 = INT64_MAX;
+                    uint32_t rf = 0, pf = 1;
+                    const uint64_t c_f0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                    for (;;) {
+                        ++n_find;
+                        ts = uni(ts); wb = uni(wb); guard = uni(guard); q1 = uni(q1);
+                        if (ts > hi || spin()) break;
+                        if (ts >= wb + 192) {                         // far ahead: refill the window
+                            wb = lo + ((ts - lo) & ~(int64_t)63);
+                            tA = tab(wb + lane); tB = tab(wb + 64 + lane); tC = tab(wb + 128 + lane);
                         }
-                        const SW2 s0 = sw_unpack(sa, sb, sc);
-                        const int64_t C = s0.b1_start == W ? (int64_t)s0.b1_cnt : 0;
-                        if (thr_w != W || C < thr_c || C - thr_c > 63) { thr_build(W, C); ++n_tk; }
-                        Q1 = (int64_t)readlane64((uint64_t)thr1, (uint32_t)(C - thr_c));
-                        Q2 = (int64_t)readlane64((uint64_t)thr2, (uint32_t)(C - thr_c));
-                        if (W + w - 1 < lim_t) lim_t = W + w - 1;
-                    }
-                    // one 64-ms view: what the state grants per ms (q), the first candidate
-                    auto view = [&](int64_t tb, const uint2 e) -> bool {
-                        const int64_t t = tb + (int64_t)lane;
-                        uint32_t q;
-                        if constexpr (A == kAlgoTB) {
-                            // tb_refill per lane, its elapsed time as (tb - last) + lane (exact:
-                            // integers below 2^53), no contraction (Lua :56-58)
-                            const int64_t last = (int64_t)sb;
-                            const double el = (double)(tb - last) + (double)lane;
-                            const double x = __longlong_as_double((long long)sa) + el * L.rate_per_ms;
-                            double bal = x < L.capacity ? x : L.capacity;
-                            if (!(sc & 1u) || t > last + L.ttl_ms) bal = L.capacity;
-                            q = bal >= 2.0 ? 2u : bal >= 1.0 ? 1u : 0u;
-                        } else {
-                            q = t >= Q2 ? 2u : t >= Q1 ? 1u : 0u;
+                        while (ts >= wb + 64) {
+                            wb += 64; tA = tB; tB = tC; tC = tab(wb + 128 + lane);
                         }
-                        if (!(t >= ts && t <= lim_t)) q = 0;
-                        const uint64_t mq = __ballot(q != 0);
-                        if (mq && q1 == INT64_MAX) q1 = tb + (int64_t)__builtin_ctzll(mq);
-                        const uint32_t cnd = q >= 2u ? e.y : q == 1u ? e.x : kWalkNone;
-                        const uint64_t m = __ballot(cnd != kWalkNone);
-                        if (!m) return false;
-                        const uint32_t l = (uint32_t)__builtin_ctzll(m);
-                        rf = (uint32_t)__builtin_amdgcn_readlane((int)cnd, (int)l);
-                        const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)e.x, (int)l);
-                        pf = rf != ex ? 2u : 1u;                  // (q >= 2 and a 2-permit acquire first)
-                        tf = tb + (int64_t)l;
-                        return true;
-                    };
-                    if (view(wb, tA) || view(wb + 64, tB)) break;
-                    ts = lim_t < wb + 127 ? lim_t + 1 : wb + 128;  // (SW: the next window)
-                }
-                if (a.dbg) cyc_find += __builtin_amdgcn_s_memtime() - c_f0;
-                // (no allow before the batch ends: the rest is denied, up to the next special)
-                const uint32_t cs = tf == INT64_MIN ? f.n_chunks - 1u : rf / kHotChunk;
-                const uint32_t cfl = 13u | ((pc - 1u) << 4) | (pofs << 8);   // cc's verdict, pc > 0
-                const uint64_t c_c0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-                if (spn <= cs || tf == INT64_MIN) {               // a special in (cc, cs] / the end
-                    enter(cc & ~63u);
-                    const uint32_t fl = pc ? cfl : deny_fl(q1);
-                    if (cb + lane == cc) { vA = ka; vB = kb; vC = kc; vF = fl; }
-                    const uint32_t e = spn <= cs ? spn : f.n_chunks;
-                    deny(cc + 1, e, sa, sb, sc, q1);
-                    if (e == f.n_chunks) break;
-                    dc = spn;
-                    continue;
-                }
-                if (cs == cc && pc > 0) {                         // another allow in the cursor chunk
-                    if (pc == 4) { undo_cursor(); dc = cc; continue; }
-                } else if (cs > cc) {
-                    const uint32_t fl = pc ? cfl : deny_fl(q1);
-                    if (cc >= cb && cs < cb + 64) {               // (the common case: one block)
-                        const uint32_t c = cb + lane;
-                        const uint32_t dfl = deny_fl(q1);
-                        if (c == cc) { vA = ka; vB = kb; vC = kc; vF = fl; }
-                        else if (c > cc && c < cs) { vA = sa; vB = sb; vC = sc; vF = dfl; }
-                    } else {
+                        int64_t lim_t = hi;                           // SW: the window's end - 1
+                        int64_t Q1 = 0, Q2 = 0;                       // SW: the window's thresholds
+                        if constexpr (A == kAlgoSW) {
+                            const int64_t w = L.window_ms;
+                            if (!(ts >= W && ts - W < w)) {
+                                int64_t rr;
+                                W = uni(jdiv(ts, w, L.inv_window, &rr) * w);
+                            }
+                            const SW2 s0 = sw_unpack(sa, sb, sc);
+                            const int64_t C = s0.b1_start == W ? (int64_t)s0.b1_cnt : 0;
+                            if (thr_w != W || C < thr_c || C - thr_c > 63) { thr_build(W, C); ++n_tk; }
+                            Q1 = (int64_t)readlane64((uint64_t)thr1, (uint32_t)(C - thr_c));
+                            Q2 = (int64_t)readlane64((uint64_t)thr2, (uint32_t)(C - thr_c));
+                            if (W + w - 1 < lim_t) lim_t = W + w - 1;
+                        }
+                        // one 64-ms view: what the state grants per ms (q), the first candidate
+                        auto view = [&](int64_t tb, const uint2 e) -> bool {
+                            const int64_t t = tb + (int64_t)lane;
+                            uint32_t q;
+                            if constexpr (A == kAlgoTB) {
+                                // tb_refill per lane, its elapsed time as (tb - last) + lane (exact:
+                                // integers below 2^53), no contraction (Lua :56-58)
+                                const int64_t last = (int64_t)sb;
+                                const double el = (double)(tb - last) + (double)lane;
+                                const double x = __longlong_as_double((long long)sa) + el * L.rate_per_ms;
+                                double bal = x < L.capacity ? x : L.capacity;
+                                if (!(sc & 1u) || t > last + L.ttl_ms) bal = L.capacity;
+                                q = bal >= 2.0 ? 2u : bal >= 1.0 ? 1u : 0u;
+                            } else {
+                                q = t >= Q2 ? 2u : t >= Q1 ? 1u : 0u;
+                            }
+                            if (!(t >= ts && t <= lim_t)) q = 0;
+                            const uint64_t mq = __ballot(q != 0);
+                            if (mq && q1 == INT64_MAX) q1 = tb + (int64_t)__builtin_ctzll(mq);
+                            const uint32_t cnd = q >= 2u ? e.y : q == 1u ? e.x : kWalkNone;
+                            const uint64_t m = __ballot(cnd != kWalkNone);
+                            if (!m) return false;
+                            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                            rf = (uint32_t)__builtin_amdgcn_readlane((int)cnd, (int)l);
+                            const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)e.x, (int)l);
+                            pf = rf != ex ? 2u : 1u;                  // (q >= 2 and a 2-permit acquire first)
+                            tf = tb + (int64_t)l;
+                            return true;
+                        };
+                        if (view(wb, tA) || view(wb + 64, tB)) break;
+                        ts = lim_t < wb + 127 ? lim_t + 1 : wb + 128;  // (SW: the next window)
+                    }
+                    if (a.dbg) cyc_find += __builtin_amdgcn_s_memtime() - c_f0;
+                    // (no allow before the batch ends: the rest is denied, up to the next special)
+                    const uint32_t cs = tf == INT64_MIN ? f.n_chunks - 1u : rf / kHotChunk;
+                    const uint32_t cfl = 13u | ((pc - 1u) << 4) | (pofs << 8);   // cc's verdict, pc > 0
+                    const uint64_t c_c0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                    if (spn <= cs || tf == INT64_MIN) {               // a special in (cc, cs] / the end
                         enter(cc & ~63u);
-                        const uint32_t fl2 = pc ? cfl : deny_fl(q1);
-                        if (cb + lane == cc) { vA = ka; vB = kb; vC = kc; vF = fl2; }
-                        deny(cc + 1, cs, sa, sb, sc, q1);
+                        const uint32_t fl = pc ? cfl : deny_fl(q1);
+                        if (cb + lane == cc) { vA = ka; vB = kb; vC = kc; vF = fl; }
+                        const uint32_t e = spn <= cs ? spn : f.n_chunks;
+                        deny(cc + 1, e, sa, sb, sc, q1);
+                        if (e == f.n_chunks) { done = true; break; }
+                        dc = spn;
+                        break;
                     }
-                    cc = cs; ka = sa; kb = sb; kc = sc; pc = 0; pofs = 0;
+                    if (cs == cc && pc > 0) {                         // another allow in the cursor chunk
+                        if (pc == 4) { undo_cursor(); dc = cc; break; }
+                    } else if (cs > cc) {
+                        const uint32_t fl = pc ? cfl : deny_fl(q1);
+                        if (cc >= cb && cs < cb + 64) {               // (the common case: one block)
+                            const uint32_t c = cb + lane;
+                            const uint32_t dfl = deny_fl(q1);
+                            if (c == cc) { vA = ka; vB = kb; vC = kc; vF = fl; }
+                            else if (c > cc && c < cs) { vA = sa; vB = sb; vC = sc; vF = dfl; }
+                        } else {
+                            enter(cc & ~63u);
+                            const uint32_t fl2 = pc ? cfl : deny_fl(q1);
+                            if (cb + lane == cc) { vA = ka; vB = kb; vC = kc; vF = fl2; }
+                            deny(cc + 1, cs, sa, sb, sc, q1);
+                        }
+                        cc = cs; ka = sa; kb = sb; kc = sc; pc = 0; pofs = 0;
+                    }
+                    const uint64_t c_a0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
+                    if (a.dbg) cyc_close += c_a0 - c_c0;
+                    pofs |= (rf % kHotChunk) << (6 * pc);
+                    ++pc;
+                    // the allow (Lua :61-64 / SlidingWindowRateLimiter :114-116) at ms tf
+                    bool burst;
+                    if constexpr (A == kAlgoTB) {
+                        const double nt = uni(tb_refill(L, tf, sa, sb, sc) - (double)pf);
+                        sa = (uint64_t)__double_as_longlong(nt);
+                        sb = (uint64_t)tf;
+                        sc = 1;
+                        burst = nt >= 1.0;                            // (elapsed 0: the balance is nt)
+                    } else {
+                        SWGeo gl{};
+                        gl.curr_start = W;
+                        sw_commit_allows(L, gl, sa, sb, sc, 1u, tf);
+                        sa = uni(sa); sb = uni(sb); sc = uni(sc);
+                        // the window's table at the new count, when it holds it
+                        const int64_t C = (int64_t)sw_unpack(sa, sb, sc).b1_cnt;
+                        if (thr_w == W && C >= thr_c && C - thr_c <= 63)
+                            burst = tf >= (int64_t)readlane64((uint64_t)thr1, (uint32_t)(C - thr_c));
+                        else
+                            burst = allowed1(tf);
+                    }
+                    if (lane == 0) ++n_allowed;
+                    ++n_changed;
+                    ++n_walk;
+                    ts = tf + 1;
+                    if (a.dbg) cyc_allow += __builtin_amdgcn_s_memtime() - c_a0;
+                    if (burst) {                                      // the next request of ms tf too: detail
+                        undo_cursor();
+                        dc = cc;
+                        break;
+                    }
                 }
-                const uint64_t c_a0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0;
-                if (a.dbg) cyc_close += c_a0 - c_c0;
-                pofs |= (rf % kHotChunk) << (6 * pc);
-                ++pc;
-                // the allow (Lua :61-64 / SlidingWindowRateLimiter :114-116) at ms tf
-                bool burst;
-                if constexpr (A == kAlgoTB) {
-                    const double nt = uni(tb_refill(L, tf, sa, sb, sc) - (double)pf);
-                    sa = (uint64_t)__double_as_longlong(nt);
-                    sb = (uint64_t)tf;
-                    sc = 1;
-                    burst = nt >= 1.0;                            // (elapsed 0: the balance is nt)
-                } else {
-                    SWGeo gl{};
-                    gl.curr_start = W;
-                    sw_commit_allows(L, gl, sa, sb, sc, 1u, tf);
-                    sa = uni(sa); sb = uni(sb); sc = uni(sc);
-                    // the window's table at the new count, when it holds it
-                    const int64_t C = (int64_t)sw_unpack(sa, sb, sc).b1_cnt;
-                    if (thr_w == W && C >= thr_c && C - thr_c <= 63)
-                        burst = tf >= (int64_t)readlane64((uint64_t)thr1, (uint32_t)(C - thr_c));
-                    else
-                        burst = allowed1(tf);
-                }
-                if (lane == 0) ++n_allowed;
-                ++n_changed;
-                ++n_walk;
-                ts = tf + 1;
-                if (burst) {                                      // the next request of ms tf too: detail
-                    undo_cursor();
-                    dc = cc;
-                }
-                if (a.dbg) cyc_allow += __builtin_amdgcn_s_memtime() - c_a0;
+                if (done) break;
             }
             flush();
             if (guard == 0 && lane == 0) atomicAdd(&a.ctl->cap_err, 1ULL);
