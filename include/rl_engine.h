@@ -225,13 +225,15 @@ int  rl_sync(rl_engine* e);
  * measurement-only kernel variants whose results are NOT valid (0 = product path);
  * "hot_threshold" (records per region for the hot-key chains, 0 = off), "route" (two-pass
  * tables: the previous batch's hot regions skip the second partition pass, default 1),
- * "region_order" (largest regions dispatched first, default 1), "sparse_max",
- * "stage_timing", "debug_regions" and the "*_per_cu" grid sizes. Every setting gives the same decisions. "fail_batches" = k makes the next k batch
+ * "region_order" (largest regions dispatched first, default 1), "walk" (the hot chains' allow
+ * walk, default 1), "walk_min" (keys walked: at least this many allows expected per batch,
+ * default 4000), "sparse_max", "stage_timing", "debug_regions" and the "*_per_cu" grid sizes.
+ * Every setting gives the same decisions. "fail_batches" = k makes the next k batch
  * calls fail with RL_E_DEVICE before enqueuing anything (tests of callers' error paths). */
 int  rl_tune(rl_engine* e, const char* key, int64_t value);
 /* Diagnostics (not needed by callers). "region_times": after a batch run with
- * rl_tune("debug_regions", 1), copies per-bin {t_start, t_end, records, rounds,
- * 4 cycle counters} (uint64 x8; s_memrealtime ticks; rounds bit 63 = a hot region).
+ * rl_tune("debug_regions", 1), copies per-bin {t_start, t_end, records, rounds, cycle
+ * counters} (uint64 x28 per bin; s_memrealtime ticks; rounds bit 63 = a hot region).
  * Returns the number of bins copied (>= 0) or a status < 0. */
 int  rl_debug_fetch(rl_engine* e, const char* what, void* out, size_t bytes);
 const char* rl_strerror(int status);
