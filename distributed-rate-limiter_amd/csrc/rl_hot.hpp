@@ -347,6 +347,13 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
             uint64_t w[8];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
+                if (k == 1 && !two) {                     // (wave-uniform) no second key: its words
+                    const uint64_t no = w[2] >> 24;       // hold only key 0's rest count
+                    w[4] = (uint64_t)INT64_MAX; w[5] = (uint64_t)INT64_MIN;
+                    w[6] = no << 24; w[7] = no << 8;
+                    gfl[1] |= no ? 8u : 0u;
+                    break;
+                }
                 const bool hot = k ? hot1 : hot0;
                 const bool early = hot && acq && tb && (int64_t)q.permits > maxp;
                 const bool plain = hot && acq && !early;
