@@ -222,14 +222,17 @@ hipError_t launch_route_next(const HotInfo* hot_info, const uint32_t* hot_count,
 __global__ __launch_bounds__(256) void k_walk_init(RegionArgs a) {
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     const int64_t lo = batch_lo(a.ctl), hi = batch_hi(a.ctl);
-    const size_t n = (size_t)2 * min(hc, walk_regions(lo, hi)) * walk_stride(lo, hi);
+    const uint32_t nreg = min(hc, walk_regions(lo, hi));
+    const uint32_t per_reg = walk_stride(lo, hi);    // uint4 per region: 2 tables of stride entries
+    const uint32_t parts = (per_reg + 4095) / 4096;  // (work units of 4096 uint4)
     const uint4 none = make_uint4(kWalkNone, kWalkNone, kWalkNone, kWalkNone);
-    uint4* t = (uint4*)a.walk_tab;                   // (strides are multiples of 64 entries)
-    const size_t stride2 = (size_t)2 * walk_stride(lo, hi);
-    for (size_t k = (size_t)blockIdx.x * 256 + threadIdx.x; k < n / 2; k += (size_t)gridDim.x * 256) {
-        const uint32_t i = (uint32_t)(2 * k / stride2);   // listed region (tables of walked keys only)
+    for (uint32_t u = blockIdx.x; u < nreg * parts; u += gridDim.x) {
+        const uint32_t i = u / parts, p = u % parts;  // listed region: tables of walked keys only
         const HotInfo& f = a.hot_info[i];
-        if (walk_dense(f, a.lims[a.region_lim[f.bin]], lo, hi, a.walk_min)) t[k] = none;
+        if (!walk_dense(f, a.lims[a.region_lim[f.bin]], lo, hi, a.walk_min)) continue;
+        uint4* t = (uint4*)a.walk_tab + (size_t)i * per_reg;
+        const uint32_t e = min(per_reg, (p + 1) * 4096);
+        for (uint32_t k = p * 4096 + threadIdx.x; k < e; k += 256) t[k] = none;
     }
 }
 
