@@ -83,3 +83,28 @@ def test_walk_two_pass_routed():
     lims = [[rl_amd.TB, 1000, 60_000, 100.0], [rl_amd.SW, 100, 1_000, 0.0]]
     tr = hot_trace(48, 2_000_000, 400_000, 0.5, [0, 1], 60_000, permits_max=2, hot_keys=2)
     both(lims, tr, batches=3, capacity=1 << 21, tune={"hot_threshold": 16384})
+
+
+@pytest.mark.parametrize("algo", ["sw", "tb"])
+def test_walk_two_keys_one_region(algo):
+    # two heavy keys in one region (chains of the dominant and the second key, slots 2 i and
+    # 2 i + 1 of the walk tables), light keys beside them, peeks / resets of every key
+    from test_gpu_hot import NS, T0, same_region_keys
+    lims = [[rl_amd.SW, 500, 30_000, 0.0]] if algo == "sw" else [[rl_amd.TB, 40, 30_000, 6.0]]
+    n = 1_500_000
+    rng = np.random.default_rng(60)
+    same = same_region_keys(6, 10, 61)                     # capacity 2^17: 2^10 regions
+    keys = rl_amd.mix64(rng.integers(0, 100_000, n).astype(np.uint64) + np.uint64(9 << 40))
+    u = rng.random(n)
+    keys[u < 0.30] = same[0]
+    keys[(u >= 0.30) & (u < 0.50)] = same[1]
+    light = (u >= 0.50) & (u < 0.51)
+    keys[light] = same[2 + rng.integers(0, 4, int(light.sum()))]
+    now = (T0 * NS + np.sort(rng.integers(0, 90_000 * NS, n))).astype(np.int64)
+    permits = rng.integers(1, 3, n).astype(np.int32)
+    op = np.zeros(n, np.uint8)
+    v = rng.random(n)
+    op[v < 0.002] = 1
+    op[v < 0.0005] = 2
+    tr = (keys, permits, now, np.zeros(n, np.uint16), op)
+    both(lims, tr, batches=3, capacity=1 << 17)
