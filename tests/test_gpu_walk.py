@@ -19,11 +19,20 @@ from test_gpu_parity import assert_same
 pytestmark = pytest.mark.gpu
 
 
-def both(lims, tr, batches, tune=None, **kw):
-    # walk_min 0: every key dense enough is walked, not only those expecting >= 4000 allows
+def both(lims, tr, batches, tune=None, walks=True, **kw):
+    # walk_min 0: every key dense enough is walked, not only those expecting >= 4000 allows.
+    # The last batch's per-region debug words (rl_tune debug_regions; word 20 = walked allows)
+    # show whether the walk ran: `walks` says whether it must have (it never may with walk 0).
     for walk in (1, 0):
-        got, want, _ = run(lims, tr, batches=batches, tune=dict(tune or {}, walk=walk, walk_min=0), **kw)
+        got, want, e = run(lims, tr, batches=batches,
+                           tune=dict(tune or {}, walk=walk, walk_min=0, debug_regions=1), **kw)
         assert_same(got, want, f"walk={walk}")
+        walked = int(e.debug_region_times(1 << 16)[:, 20].sum())
+        if walk and walks:
+            assert walked > 0, "the walk did not run"
+        else:
+            assert walked == 0, f"walk={walk}: {walked} walked allows"
+
 
 
 @pytest.mark.parametrize("permits_max", [1, 2])
@@ -65,10 +74,10 @@ def test_walk_off_for_large_permits_and_regression():
     # the chains stay on the chunk path, results unchanged
     lims = [[rl_amd.TB, 500, 30_000, 50.0], [rl_amd.SW, 300, 5_000, 0.0]]
     tr = hot_trace(45, 1_200_000, 10_000, 0.6, [0, 1], 40_000, permits_max=4, hot_keys=2)
-    both(lims, tr, batches=2, capacity=1 << 15)
+    both(lims, tr, batches=2, capacity=1 << 15, walks=False)
     lims = [[rl_amd.TB, 300, 20_000, 30.0]]
     tr = hot_trace(46, 1_200_000, 10_000, 0.6, [0], 40_000, permits_max=2, regress=True)
-    both(lims, tr, batches=2, capacity=1 << 15)
+    both(lims, tr, batches=2, capacity=1 << 15, walks=False)
 
 
 def test_walk_tb_early_rejects():
