@@ -2,9 +2,10 @@
 """CPU model of the hot chains' allow walk (rl_hot.hpp `walk`, k_hot_summ's per-ms table,
 k_hot_fill's walk verdicts) for ONE key's record stream, checked against the sequential
 semantics (SlidingWindowRateLimiter.java:85-180, TokenBucketRateLimiter Lua :38-68) record by
-record. It mirrors the device loop step for step (cursor chunk, pending allow, 128-ms table
-views, bursts, conflicts, specials), so a logic error or a loop that does not end shows up
-here instead of on the GPU. Test tooling only: nothing in the product imports it.
+record. It mirrors the device loop step for step (cursor chunk with up to 4 pending allows,
+remaining-0 chunks, bursts, fifth allows, specials; the device's 64-ms table views are one
+loop over ms here), so a logic error or a loop that does not end shows up here instead of on
+the GPU (tests/test_walk_model.py runs it). Test tooling only: nothing in the product imports it.
 
 usage: tools/walk_model.py [--algo sw|tb] [--n N] [--rate R] [--seed S] [--specials F]
 """
