@@ -114,6 +114,22 @@ _WALK_TAB_ENTRIES = 1 << 26                # rl_launch.hpp kWalkTabEntries (uint
 _ROUTER_EXC = 4096                     # rl_router.cpp kExcCap
 
 
+_WALK_MIN_ALLOWS, _WALK_SPAN_MS = 4000, 1 << 17   # rl_launch.hpp kWalkMinAllows / kWalkSpan
+
+
+def walk_possible(cfg):
+    """Could a key of this config be walked (rl_hot.hpp walk_dense: at least kWalkMinAllows
+    expected allows over a batch's span)? The engine holds the 512-MiB walk tables only then."""
+    span = cfg["span_ns"] / NS
+    if span >= _WALK_SPAN_MS:
+        return False
+    for algo, mx, w, refill in cfg["limiters"]:
+        e = mx + refill / 1000.0 * span if algo == rl_amd.TB else mx * (span / w + 2.0)
+        if e >= _WALK_MIN_ALLOWS:
+            return True
+    return False
+
+
 def engine_max_batch(n, ws, router="capi"):
     """max_batch of a rank's engine in run(): its per-exchange receive capacity."""
     return n * ws if (ws > 1 and router == "python") else n * min(ws, 2)
@@ -153,7 +169,8 @@ def hbm_footprint(name, n, ws, steps, warm, router="capi", recv_cap=0, table_sca
     out["region_arrays"] = sets * regions * 8 + regions * (4 + 4 + 1) + 4 * (regions + 1)
     l1 = m // _HOT_CHUNK + _HOT_MAX + 1
     out["hot_summaries"] = (l1 + l1 // 64 + _HOT_MAX + 1) * 8
-    out["walk_tables"] = _WALK_TAB_ENTRIES * 8     # allow-walk tables (hot path on)
+    # allow-walk tables: allocated once a batch lists a key dense enough to walk (k_hot_scan)
+    out["walk_tables"] = _WALK_TAB_ENTRIES * 8 if walk_possible(cfg) else 0
     if ws > 1 and router == "capi":
         ret = lambda t: t * 8 + ws * (8 + 8 + 16 * _ROUTER_EXC)   # ret_bound (rl_router.cpp)
         send = n * (4 + 16 + 2 + 8 + 4 + 8 + 8) + ret(n)
@@ -174,20 +191,24 @@ def dist_env():
 
 
 def load_pmc(config_name, kernel, batch, world):
-    """HBM traffic per launch from the committed rocprofv3 PMC summary
-    (profiles/pmc_summary.json, tools/pmc_json.py), or None unless that profile was taken on
-    this exact workload: the same config, requests per GPU per step and world size."""
+    """(HBM traffic per launch, the profile directory it came from) from the committed
+    rocprofv3 PMC summary (profiles/pmc_summary.json, tools/pmc_json.py), or (None, None)
+    unless that profile was taken on this exact workload: the same config, requests per GPU
+    per step and world size. The directory is the summary's _meta[config] (pmc_json always
+    records it; tests/test_pmc_provenance.py recomputes the values from it)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
-        d = json.load(open(path)).get(config_name, {})
+        s = json.load(open(path))
+        d = s.get(config_name, {})
         if d.get("batch") != batch or d.get("world", 1) != world:
-            return None
+            return None, None
         k = d.get(kernel)
-        return None if k is None else float(k["hbm_bytes_per_launch"])
+        return (None, None) if k is None else (float(k["hbm_bytes_per_launch"]),
+                                               s.get("_meta", {}).get(config_name))
     except Exception:
-        return None
+        return None, None
 
 
 def config1_line(dev):
@@ -446,7 +467,7 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
     step_s = elapsed / steps
     achieved = algo_bytes * ws / step_s / 1e9             # whole node
     peak = HBM_PEAK_GBS * ws
-    traffic = load_pmc(name, "step", n, ws)
+    traffic, traffic_dir = load_pmc(name, "step", n, ws)
     res_b = eng.result_width()
     kernels = {}
     n_normal = n - warm_stats["routed"] if warm > 1 else n
@@ -482,7 +503,8 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "traffic_source": None if traffic is None else
-                     f"profiles/pmc_summary.json[{name}] (same config, {n} requests/GPU, world {ws})",
+                     f"{traffic_dir} (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this config, {n} "
+                     f"requests/GPU, world {ws}; folded into profiles/pmc_summary.json[{name}])",
                      "kernel": "pipeline (one step)",
                      "algorithmic_bytes_per_step": algo_bytes,
                      "bytes_per_request": req_bytes, "distinct_keys_per_step": U,

@@ -105,6 +105,8 @@ struct rl_engine {
     size_t hot_summ_cap = 0, hot_summ_l1 = 0;
     uint2* walk_tab = nullptr;              // [kWalkTabEntries] allow-walk tables (hot chains)
     bool walk = true;                       // rl_tune("walk"): allow walks in the hot chains
+    uint32_t walk_hint = 0;                 // listed regions that wanted a walk in the last batch
+                                            // seen complete (walk_tab is allocated once it is > 0)
     uint32_t walk_min = kWalkMinAllows;     // rl_tune("walk_min"): fewest expected allows walked
     uint32_t* hot_mark = nullptr;           // [hot_mark_cap] epoch marks per bin
     size_t hot_mark_cap = 0;
@@ -159,6 +161,7 @@ struct rl_engine {
     bool timing = false;
     bool last_wide = false;
     bool pending_status = false;
+    bool enqueued = false;                  // the last engine call enqueued a batch (d_ctl is its)
     uint32_t hot_hint = 0xFFFFFFFFu;        // hot regions of the last batch seen complete
     int last_status = RL_OK;
     uint64_t last_n = 0;
@@ -224,6 +227,7 @@ extern "C" const char* rl_strerror(int s) {
         case RL_E_NOMEM: return "out of memory";
         case RL_E_TOO_LARGE: return "batch larger than max_batch";
         case RL_E_LIMITERS: return "too many limiters";
+        case RL_E_INTERNAL: return "internal error (engine logic)";
         default: return "unknown status";
     }
 }
@@ -590,6 +594,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (n > e->opts.max_batch) return RL_E_TOO_LARGE;
     e->last_n = n;
     e->pending_status = false;
+    e->enqueued = false;
     e->last_status = RL_OK;
     if (n == 0) return RL_OK;
     if (!key || !permits || !now_ns || !allowed || !remaining) return RL_E_INVALID_ARG;
@@ -660,8 +665,14 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (hot) {
         rc = ensure_hot_mark(e, n_bins);
         if (rc == RL_OK) rc = ensure_hot_summ(e, n);
-        if (rc == RL_OK && e->walk && !e->walk_tab) rc = dalloc(&e->walk_tab, kWalkTabEntries);
         if (rc != RL_OK) return rc;
+        // Allow-walk tables (512 MiB): only once a batch had a key dense enough to walk
+        // (k_hot_scan's count; a workload that never walks, such as tb_uniform, holds none).
+        // The walk is optional and decides identically: a failed allocation turns it off.
+        if (e->walk && !e->walk_tab && e->walk_hint > 0 && dalloc(&e->walk_tab, kWalkTabEntries) != RL_OK) {
+            std::fprintf(stderr, "rl_engine: no device memory for the allow-walk tables; walks off\n");
+            e->walk = false;
+        }
         if (++e->epoch == 0) {                       // marks hold epochs: restart after wrap
             HIP_OK(hipMemsetAsync(e->hot_mark, 0, e->hot_mark_cap * sizeof(uint32_t), s));
             e->epoch = 1;
@@ -837,6 +848,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         e->next_set ^= 1;
     }
     e->pending_status = true;
+    e->enqueued = true;
     return RL_OK;
 }
 
@@ -851,11 +863,12 @@ static void apply_growth(rl_engine* e, const unsigned long long (&grow)[4], bool
     }
 }
 
-static int status_of(bool invalid, bool cap_err, bool span_overflow) {
+static int status_of(bool invalid, bool cap_err, bool span_overflow, bool internal) {
     int st = RL_OK;
     if (invalid) st = RL_E_INVALID_REQUEST;
     if (cap_err) st = RL_E_CAPACITY;
     if (span_overflow) st = RL_E_INVALID_ARG;
+    if (internal) st = RL_E_INTERNAL;
     return st;
 }
 
@@ -866,7 +879,8 @@ static int collect_status(rl_engine* e) {
     e->pending_status = false;
     BatchCtl& c = *e->h_ctl;
     e->hot_hint = c.n_hot;
-    const int st = status_of(c.invalid != 0, c.cap_err != 0, c.span_overflow != 0);
+    e->walk_hint = c.n_walk;
+    const int st = status_of(c.invalid != 0, c.cap_err != 0, c.span_overflow != 0, c.internal_err != 0);
     e->last_status = st;
     apply_growth(e, c.grow, c.cap_err != 0);
     c.grow[0] = c.grow[1] = c.grow[2] = c.grow[3] = 0;
@@ -878,7 +892,12 @@ int engine_status_accum(rl_engine* e, unsigned long long* acc, void* stream) {
     if (!e || !acc) return RL_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(e->mu);
     const BatchScratch& B = e->sc[e->pipeline ? e->next_set ^ 1 : 0];   // the last batch's set
-    HIP_OK(launch_status_accum(B.d_ctl, acc, stream ? (hipStream_t)stream : e->stream));
+    // A call that enqueued no batch (nothing received in this round, or a status set on the
+    // host) leaves d_ctl holding an earlier batch whose status and growth were already
+    // applied: fold only the host-side status then.
+    const unsigned long long host = e->last_status == RL_E_INVALID_REQUEST ? 1ULL : 0ULL;
+    HIP_OK(launch_status_accum(e->enqueued ? B.d_ctl : nullptr, e->enqueued ? 0ULL : host, acc,
+                               stream ? (hipStream_t)stream : e->stream));
     return RL_OK;
 }
 
@@ -889,8 +908,8 @@ int engine_status_settle(rl_engine* e, const unsigned long long* acc) {
     if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
     // the last batch's own status is part of acc: it must not be collected (grown) again
     e->pending_status = false;
-    e->hot_hint = e->h_ctl->n_hot;
-    const int st = status_of(acc[0] & 1u, acc[0] & 2u, acc[0] & 4u);
+    if (e->enqueued) { e->hot_hint = e->h_ctl->n_hot; e->walk_hint = e->h_ctl->n_walk; }
+    const int st = status_of(acc[0] & 1u, acc[0] & 2u, acc[0] & 4u, acc[0] & 8u);
     e->last_status = st;
     const unsigned long long grow[4] = {acc[1], acc[2], acc[3], acc[4]};
     apply_growth(e, grow, (acc[0] & 2u) != 0);
@@ -1151,6 +1170,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "walk") == 0) {              // allow walks of the hot chains
         e->walk = value != 0;
+        if (!e->walk && e->walk_tab) {                 // (hipFree waits for the batches in flight)
+            HIP_OK(hipStreamSynchronize(e->stream));
+            if (e->hstream) HIP_OK(hipStreamSynchronize(e->hstream));
+            dfree(e->walk_tab);
+        }
         return RL_OK;
     }
     if (std::strcmp(key, "walk_min") == 0) {          // keys walked: at least this many allows expected
@@ -1171,7 +1195,10 @@ extern "C" int rl_sync(rl_engine* e) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_OK(hipStreamSynchronize(e->stream));
     if (e->pstream) HIP_OK(hipStreamSynchronize(e->pstream));
-    if (e->pending_status) e->hot_hint = e->h_ctl->n_hot;    // the last batch is complete
+    if (e->pending_status) {                                 // the last batch is complete
+        e->hot_hint = e->h_ctl->n_hot;
+        e->walk_hint = e->h_ctl->n_walk;
+    }
     return RL_OK;
 }
 

@@ -21,6 +21,13 @@ __global__ __launch_bounds__(1024) void k_hot_scan(RegionArgs a) {
         a.hot_info[t].group_base = ex2;
     }
     if (t == 0) { a.hot_total[0] = tot; a.hot_total[1] = tot2; }
+    // listed regions whose key could be walked (walk_table_on without the table): the host
+    // allocates the walk tables only once a batch has one (tb_uniform never does)
+    const int64_t lo = batch_lo(a.ctl), hi = batch_hi(a.ctl);
+    const bool wants = t < hc && t < walk_regions(lo, hi) &&
+                       walk_dense(a.hot_info[t], a.lims[a.region_lim[a.hot_info[t].bin]], lo, hi, a.walk_min);
+    const uint32_t nw = (uint32_t)__syncthreads_count(wants);
+    if (t == 0) a.ctl->n_walk = nw;
 }
 
 // Hot-region selection, largest first: k_hot_hist counts the bins at or above the

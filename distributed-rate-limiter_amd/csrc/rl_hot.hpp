@@ -535,6 +535,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     const uint32_t rest_w = hot_ok2 ? 7u : 3u;
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_detail = 0, n_other = 0;
+    uint32_t n_internal = 0;                          // walk logic errors (RL_E_INTERNAL, uniform)
     uint32_t n_changed = 0, n_tk = 0, n_fb = 0;       // debug: changes, [T0, T1) updates,
     uint32_t n_late = 0;                              // detailed chunks starting before T0 / ending past T1
     uint32_t n_prehit = 0;                            // debug: chunks whose records were prefetched
@@ -1148,6 +1149,9 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             uint32_t pc = 0, pofs = 0;                        // cc's walked allows: count, offsets
             int64_t ts = lo;                                  // the next allow is at ms >= ts
             bool must = false;                                // cc must be detailed (see detail_at)
+            // the latest ms of the key's plain acquires in the chunks detail_at has passed
+            // (the boundary ms whose later acquires the table cannot show; INT64_MIN: none)
+            int64_t mlast = INT64_MIN;
             int64_t W = 0;                                    // SW: the window of the thresholds in use
             if constexpr (A == kAlgoSW) {
                 int64_t rr;
@@ -1160,6 +1164,22 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 if (guard != 0) --guard;
                 return guard == 0;
             };
+            // The latest ms of the key's plain acquires in the chunks before c (INT64_MIN: none),
+            // from the records themselves (the summaries of decided chunks hold verdicts by
+            // now). Plain acquires are in time order (k_hot_summ's flags), so it is the last
+            // one found going back. Only after a chunk whose key records are specials alone.
+            auto plain_before = [&](uint32_t c) -> int64_t {
+                for (uint32_t k = c; k-- > 0;) {
+                    const uint32_t j = f.start + k * kHotChunk + lane;
+                    const bool valid = j < f.end;
+                    const Req q = Codec::dec(recs[valid ? j : f.start], base);
+                    const bool plain = is_key(q, valid) && q.op == (uint32_t)kOpAcquire &&
+                                       !(A == kAlgoTB && (int64_t)q.permits > L.max_permits);
+                    const uint64_t m = __ballot(plain);
+                    if (m) return uni((int64_t)readlane64((uint64_t)q.now_ms, 63u - (uint32_t)__builtin_clzll(m)));
+                }
+                return INT64_MIN;
+            };
             // a chunk detailed from the current state (the group walk's path), then the cursor past it
             auto detail_at = [&](uint32_t c) {
                 T0 = hot_t0<A>(lo, hi, sa, sb, sc);
@@ -1170,12 +1190,23 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 int64_t mxc;
                 cinfo(c, w2, mxc);
                 cc = c + 1; ka = sa; kb = sb; kc = sc; pc = 0; pofs = 0;
-                // the next chunk's acquires in the last ms of this one come after every table
-                // entry of that ms in this chunk: if the state still grants there, detail it too
-                if (mxc != INT64_MIN) {
-                    if (mxc + 1 > ts) ts = mxc + 1;
-                    must = uni((uint32_t)allowed1(mxc)) != 0u;
+                const bool special = (w2 & 0xFFu) != 0u;
+                // the boundary: this chunk's last plain acquire, else (specials only) the last
+                // one before it; a chunk without the key's records (reached as a `must` chunk
+                // right after the boundary's own) leaves it as it is
+                if (mxc != INT64_MIN) mlast = mxc;
+                else if (special) mlast = plain_before(c);
+                mlast = uni(mlast);
+                if (special) {
+                    // a reset may grant acquires the old state denied: the search starts again
+                    // right after the boundary (every later plain acquire is at or after it)
+                    ts = mlast == INT64_MIN ? lo : mlast + 1;
+                } else if (mlast != INT64_MIN && mlast + 1 > ts) {
+                    ts = mlast + 1;
                 }
+                // the next chunks' acquires in the boundary ms come after every table entry of
+                // that ms: while the state grants there, the next chunk is detailed too
+                must = mlast != INT64_MIN && uni((uint32_t)allowed1(mlast)) != 0u;
             };
             // back to the cursor chunk's start state, to detail it (the detail counts its
             // walked allows again)
@@ -1222,7 +1253,8 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         ++n_find;
                         ts = uni(ts); wb = uni(wb); guard = uni(guard); q1 = uni(q1);
                         if (ts > hi || spin()) break;
-                        if (ts >= wb + 192) {                         // far ahead: refill the window
+                        if (ts < wb || ts >= wb + 192) {              // far ahead (or searched again
+                                                                      // after a special): refill the window
                             wb = lo + ((ts - lo) & ~(int64_t)63);
                             tA = tab(wb + lane); tB = tab(wb + 64 + lane); tC = tab(wb + 128 + lane);
                         }
@@ -1291,6 +1323,15 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                         dc = spn;
                         break;
                     }
+                    if (cs < cc) {
+                        // a table entry in a decided chunk: the search bound (ts above every
+                        // plain acquire before the cursor) excludes it, so this is a logic
+                        // error; the batch reports RL_E_INTERNAL and the cursor is detailed
+                        ++n_internal;
+                        if (pc > 0) undo_cursor();
+                        dc = cc;
+                        break;
+                    }
                     if (cs == cc && pc > 0) {                         // another allow in the cursor chunk
                         if (pc == 4) { undo_cursor(); dc = cc; break; }
                     } else if (cs > cc) {
@@ -1346,7 +1387,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
                 if (done) break;
             }
             flush();
-            if (guard == 0 && lane == 0) atomicAdd(&a.ctl->cap_err, 1ULL);
+            if (guard == 0) ++n_internal;                // the step bound: a walk that would not end
             if (a.dbg) cyc_walk += __builtin_amdgcn_s_memtime() - c_w0;
             wave_fence();
             if (lane == 0) { S.sa[hs] = sa; S.sb[hs] = sb; S.sc[hs] = sc; }
@@ -1496,6 +1537,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         if (n_allowed) atomicAdd(st + kStAllowed, (unsigned long long)n_allowed);
         if (n_invalid) atomicAdd(st + kStInvalid, (unsigned long long)n_invalid);
         if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
+        if (n_internal) atomicOr(&a.ctl->internal_err, 1u);
     }
     // ---- write the region back, statistics
     const bool hot_touched = __any(any_hot);

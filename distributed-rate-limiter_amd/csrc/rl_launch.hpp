@@ -43,6 +43,9 @@ struct BatchCtl {
                                // batch's hot regions to bins of their own (k_route_ranges)
     uint32_t n_hot;            // hot regions of the batch (k_hot_prep): the next batches'
                                // chain-launch size hint (RegionArgs::chain_grid)
+    uint32_t internal_err;     // a kernel met a state its logic excludes (RL_E_INTERNAL)
+    uint32_t n_walk;           // listed hot regions with a key dense enough for an allow walk
+                               // (k_hot_scan): the host allocates the walk tables once it is > 0
 };
 // A region holding more than kGrowUsed live keys after a batch (or one that overflowed)
 // flags its limiter for growth (rl_engine doubles its region count at the next status
@@ -420,9 +423,11 @@ hipError_t launch_fill_header(int64_t* hdr, const int64_t* base_ovf, int64_t sta
                               hipStream_t s);
 hipError_t launch_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, int64_t rem,
                              hipStream_t s);
-// acc[0] |= status flags (1 invalid, 2 capacity, 4 span overflow), acc[1..4] |= ctl->grow
+// acc[0] |= status flags (1 invalid, 2 capacity, 4 span overflow, 8 internal) of ctl (nullable)
+// and `flags`; acc[1..4] |= ctl->grow
 constexpr uint32_t kStatusAccWords = 5;
-hipError_t launch_status_accum(const BatchCtl* ctl, unsigned long long* acc, hipStream_t s);
+hipError_t launch_status_accum(const BatchCtl* ctl, unsigned long long flags, unsigned long long* acc,
+                               hipStream_t s);
 
 // internal helpers of rl_engine.cpp for rl_router.cpp (not part of the C-ABI)
 int route_pack_wire_mm(rl_engine* e, size_t n, const uint32_t* perm, const uint64_t* key,

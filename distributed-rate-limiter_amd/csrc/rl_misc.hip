@@ -455,15 +455,21 @@ hipError_t launch_fill_value(uint8_t* allowed, int64_t* remaining, uint32_t n, i
 
 // Router split rounds: fold one engine batch's status flags and growth bits into a
 // router-owned accumulator (kStatusAccWords), so the rounds of a step need no host read.
-__global__ void k_status_accum(const BatchCtl* ctl, unsigned long long* acc) {
+// ctl == nullptr: the engine call enqueued no batch (nothing received, or a status set on the
+// host), whose flags come in `flags` alone.
+__global__ void k_status_accum(const BatchCtl* ctl, unsigned long long flags, unsigned long long* acc) {
     if (threadIdx.x != 0) return;
-    acc[0] |= (ctl->invalid ? 1ULL : 0ULL) | (ctl->cap_err ? 2ULL : 0ULL) |
-              (ctl->span_overflow ? 4ULL : 0ULL);
-    for (int i = 0; i < 4; ++i) acc[1 + i] |= ctl->grow[i];
+    if (ctl) {
+        flags |= (ctl->invalid ? 1ULL : 0ULL) | (ctl->cap_err ? 2ULL : 0ULL) |
+                 (ctl->span_overflow ? 4ULL : 0ULL) | (ctl->internal_err ? 8ULL : 0ULL);
+        for (int i = 0; i < 4; ++i) acc[1 + i] |= ctl->grow[i];
+    }
+    acc[0] |= flags;
 }
 
-hipError_t launch_status_accum(const BatchCtl* ctl, unsigned long long* acc, hipStream_t s) {
-    hipLaunchKernelGGL(k_status_accum, dim3(1), dim3(64), 0, s, ctl, acc);
+hipError_t launch_status_accum(const BatchCtl* ctl, unsigned long long flags, unsigned long long* acc,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_status_accum, dim3(1), dim3(64), 0, s, ctl, flags, acc);
     return hipGetLastError();
 }
 

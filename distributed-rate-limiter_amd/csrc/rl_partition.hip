@@ -33,6 +33,8 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
             c->table_bytes = 0;
             c->n_normal = a.n;                           // k_route_ranges lowers it when routing
             c->n_hot = 0;                                // k_hot_prep sets it when the hot path runs
+            c->internal_err = 0;
+            c->n_walk = 0;                               // k_hot_scan sets it when the hot path runs
         }
     }
     // later passes partition the normal records only (their count is on device)

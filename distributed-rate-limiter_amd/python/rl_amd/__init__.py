@@ -25,6 +25,7 @@ RL_E_DEVICE = -4
 RL_E_NOMEM = -5
 RL_E_TOO_LARGE = -6
 RL_E_LIMITERS = -7
+RL_E_INTERNAL = -8      # engine logic error (include/rl_engine.h)
 
 SW, TB = 0, 1
 OP_ACQUIRE, OP_PEEK, OP_RESET = 0, 1, 2

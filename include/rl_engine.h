@@ -63,6 +63,11 @@ extern "C" {
 #define RL_E_NOMEM            (-5)  /* device or host allocation failed */
 #define RL_E_TOO_LARGE        (-6)  /* batch larger than rl_opts.max_batch */
 #define RL_E_LIMITERS         (-7)  /* too many limiters / table space exhausted */
+#define RL_E_INTERNAL         (-8)  /* a kernel met a state its logic excludes (an engine bug,
+                                       not a capacity or input problem): the hot chains' allow
+                                       walk found an allow in a chunk it had already decided, or
+                                       exceeded its step bound. The batch's results for the keys
+                                       involved are suspect; report it as a defect. */
 
 /* ---- algorithms ---------------------------------------------------------- */
 #define RL_ALGO_SLIDING_WINDOW 0    /* algorithms/SlidingWindowRateLimiter.java */

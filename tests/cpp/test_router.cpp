@@ -116,6 +116,7 @@ static int loop_a2av(void* ctx, const void* send, const uint64_t* so, const uint
 struct Result {
     std::vector<uint8_t> a; std::vector<int64_t> r; int finish = 0; uint32_t placed = 0; int step_rc = 0;
     int fail_step = -1;               // first step whose rl_router_step returned an error
+    std::vector<int> rcs;             // every step's status
     rl_router_stats st{};
 };
 
@@ -172,6 +173,7 @@ static void run_rank(int G, int rank, Loop* loop, const Trace* tr, size_t n, int
         HIPC(hipMemcpyAsync(dl, &tr->lim[b], n * 2, hipMemcpyHostToDevice, s));
         if (st == fail_at) CHECK(rl_tune(e, "fail_batches", 1) == RL_OK);   // this rank's engine only
         const int rc = rl_router_step(r, n, dk, dp, dt, dl, da, dr, s);
+        out->rcs.push_back(rc);
         if (rc != RL_OK && out->step_rc == RL_OK) { out->step_rc = rc; out->fail_step = st; }
         // nosync_finish: the last step's work is still queued on s when finish is called
         // (finish must wait for it itself)
@@ -378,6 +380,51 @@ static void loop_error_case() {
                 res[0].finish, res[1].finish);
 }
 
+// a rank that receives nothing in every round of a split step must not
+// fold the previous batch's status again. Step 0 sends every request to owner 1 (distinct
+// keys: its one-key table overflows, RL_E_CAPACITY) in split rounds, owner 0 receiving
+// nothing; steps 1-3 send every request to owner 0 (64 keys), owner 1 receiving nothing in
+// any round. The capacity error is reported exactly once by every rank, and owner 1's table
+// grows once for it (not again for each empty step).
+static void loop_empty_rounds_case() {
+    const int G = 2;
+    const size_t n = 20000;
+    const int steps = 4;
+    const int64_t NS = 1000000, T0 = 1700000000000LL;
+    Trace tr;
+    std::vector<uint64_t> own0, own1;
+    for (uint64_t x = 1; own0.size() < 64 || own1.size() < (size_t)G * n; ++x) {
+        const uint64_t k = mix(x * 0x9E3779B97F4A7C15ULL + 11);
+        (rl_owner_of(k, 0, G) == 0 ? own0 : own1).push_back(k);
+    }
+    for (int st = 0; st < steps; ++st)
+        for (size_t i = 0; i < (size_t)G * n; ++i) {
+            tr.key.push_back(st == 0 ? own1[i] : own0[i % 64]);
+            tr.permits.push_back(1);
+            tr.now.push_back((T0 + st * 1000 + (int64_t)(i / 64)) * NS);
+            tr.lim.push_back(0);
+        }
+    Loop loop(G);
+    std::vector<Result> res(G);
+    std::vector<std::thread> th;
+    for (int rank = 0; rank < G; ++rank)
+        th.emplace_back(run_rank, G, rank, &loop, &tr, n, steps, false, (uint64_t)1, &res[rank], nullptr,
+                        false, (size_t)12000, -1);
+    for (auto& x : th) x.join();
+    for (int rank = 0; rank < G; ++rank) {
+        int cap = res[rank].finish == RL_E_CAPACITY ? 1 : 0, other = 0;
+        for (int rc : res[rank].rcs) {
+            cap += rc == RL_E_CAPACITY;
+            other += rc != RL_OK && rc != RL_E_CAPACITY;
+        }
+        CHECK(cap == 1 && other == 0);
+        // every step splits, but the one returning the fatal status did not exchange its batch
+        CHECK(res[rank].st.split_steps == (uint64_t)steps - 1);
+        std::printf("empty split rounds: rank %d step statuses %d %d %d %d, finish %d\n", rank,
+                    res[rank].rcs[0], res[rank].rcs[1], res[rank].rcs[2], res[rank].rcs[3], res[rank].finish);
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "loop";
     if (mode == "loop") {
@@ -394,6 +441,7 @@ int main(int argc, char** argv) {
         loop_nosync_finish_case();
         loop_span_case();
         loop_error_case();
+        loop_empty_rounds_case();
     } else if (mode == "rccl") {
         char id[RL_RCCL_ID_BYTES];
         CHECK(rl_rccl_unique_id(id) == RL_OK);

@@ -50,6 +50,16 @@ def test_traffic_keyed_by_workload(tmp_path, monkeypatch):
     d = json.load(open(os.path.join(bench.ROOT, "profiles", "pmc_summary.json")))
     for name in ("sw_zipf", "tb_uniform", "zipf_1b", "mixed_tenants"):
         assert d[name]["batch"] == bench.CONFIGS[name]["batch"] and d[name]["world"] == 1
-        assert bench.load_pmc(name, "step", bench.CONFIGS[name]["batch"], 1) > 0
-        assert bench.load_pmc(name, "step", bench.CONFIGS[name]["batch"], 2) is None
-        assert bench.load_pmc(name, "step", 1 << 21, 1) is None
+        v, src = bench.load_pmc(name, "step", bench.CONFIGS[name]["batch"], 1)
+        assert v > 0 and src == d["_meta"][name] and os.path.isdir(os.path.join(bench.ROOT, src))
+        assert bench.load_pmc(name, "step", bench.CONFIGS[name]["batch"], 2) == (None, None)
+        assert bench.load_pmc(name, "step", 1 << 21, 1) == (None, None)
+
+
+def test_walk_tables_only_where_a_key_can_walk():
+    # tb_uniform (and the minute-window configs) never walk, so the engine
+    # holds no walk tables for them; mixed_tenants' TB 1000 @ 100/s can
+    walks = {name: bench.walk_possible(cfg) for name, cfg in bench.CONFIGS.items()}
+    assert walks == {"tb_uniform": False, "sw_zipf": False, "zipf_1b": False, "mixed_tenants": True}
+    fp = bench.hbm_footprint("tb_uniform", 1 << 26, 1, 20, 5)
+    assert fp["walk_tables"] == 0

@@ -117,3 +117,38 @@ def test_walk_two_keys_one_region(algo):
     op[v < 0.0005] = 2
     tr = (keys, permits, now, np.zeros(n, np.uint16), op)
     both(lims, tr, batches=3, capacity=1 << 17)
+
+
+@pytest.mark.parametrize("algo", ["tb", "sw"])
+def test_walk_reset_only_chunks(algo):
+    # chunks of the walked key's region whose only record of the key is a
+    # reset, after chunks whose acquires the old state denied. Every record of the trace is in
+    # one region (6 keys), so region chunk c of a batch is records 64c .. 64c + 63 of it; in 24
+    # chunks per batch the dominant key's records are replaced by other keys' and one of its
+    # records becomes a reset. The walk must search again from the key's last plain acquire
+    # (tools/walk_model.py, tests/test_walk_model.py::test_walk_model_reset_only_chunks).
+    from test_gpu_hot import NS, T0
+    from test_gpu_hot import same_region_keys
+    lims = [[rl_amd.TB, 40, 30_000, 20.0]] if algo == "tb" else [[rl_amd.SW, 60, 2_000, 0.0]]
+    n = 1_500_000
+    rng = np.random.default_rng(64)
+    same = same_region_keys(6, 10, 65)                     # capacity 2^17: 2^10 regions
+    u = rng.random(n)
+    keys = np.where(u < 0.35, same[0], same[1 + rng.integers(0, 5, n)]).astype(np.uint64)
+    now = (T0 * NS + np.sort(rng.integers(0, 60_000 * NS, n))).astype(np.int64)
+    permits = rng.integers(1, 3, n).astype(np.int32)
+    op = np.zeros(n, np.uint8)
+    cuts = np.linspace(0, n, 3).astype(int)
+    for b in range(2):
+        nch = (cuts[b + 1] - cuts[b]) // 64
+        for c in rng.choice(np.arange(4, nch - 4), 24, replace=False):
+            j0 = cuts[b] + 64 * int(c)
+            blk = slice(j0, j0 + 64)
+            mine = keys[blk] == same[0]
+            keys[blk] = np.where(mine, same[1], keys[blk])
+            j = j0 + int(rng.integers(0, 64))
+            keys[j] = same[0]
+            op[j] = 2
+            permits[j] = 1
+    tr = (keys, permits, now, np.zeros(n, np.uint16), op)
+    both(lims, tr, batches=2, capacity=1 << 17)

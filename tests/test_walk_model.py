@@ -28,8 +28,9 @@ def _trace(seed, n, per_ms, specials, pmax):
 def _check(algo, recs, mk, w):
     want = []
     s = mk()
-    for t, p, op in recs:
-        want.append(s.step(t, p, op))
+    for r in recs:
+        mine = len(r) < 4 or r[3]
+        want.append(s.step(r[0], r[1], r[2]) if mine else None)
     stats = {"detail": 0, "allows": 0, "conflict": 0, "burst": 0}
     got = wm.walk(recs, mk(), algo, w, stats)
     bad = [j for j in range(len(recs)) if got[j] != want[j]]
@@ -64,3 +65,38 @@ def test_walk_model_dense_key_uses_remaining_zero_verdicts():
     recs = _trace(7, 20000, 40.0, 0.0, 1)
     stats = _check("tb", recs, lambda: wm.TB(1000, 100.0, 60000), 60000)
     assert stats.get("rem0", 0) > 10000 and stats["detail"] < 50
+
+
+def _sparse_trace(seed, n, per_ms, share, pmax, reset_chunks):
+    # the walked key's records (share of them) among other keys' records, as in a hot region;
+    # in `reset_chunks` random chunks the key's only record is a reset (after the acquires of
+    # the chunks before were denied under the old state)
+    rnd = random.Random(seed)
+    t0 = 1_700_000_000_000
+    span = max(1, int(n / per_ms))
+    ts = sorted(t0 + rnd.randrange(span) for _ in range(n))
+    recs = [(t, rnd.randint(1, pmax), 0, rnd.random() < share) for t in ts]
+    nch = (n + 63) // 64
+    for c in rnd.sample(range(2, nch - 2), reset_chunks):
+        for j in range(c * 64, min(n, c * 64 + 64)):
+            t, p, _, _ = recs[j]
+            recs[j] = (t, p, 0, False)
+        j = c * 64 + rnd.randrange(64)
+        recs[j] = (recs[j][0], 1, 2, True)
+    return recs
+
+
+@pytest.mark.parametrize("algo", ["tb", "sw"])
+@pytest.mark.parametrize("share", [0.5, 0.08])
+def test_walk_model_reset_only_chunks(algo, share):
+    # a chunk whose only record of the key is a reset, after chunks whose
+    # acquires were denied under the old state. The search must start again after the key's
+    # last plain acquire (not where the old state's search stopped), so that it neither allows
+    # a record of a decided chunk nor skips the acquires the reset frees; a sparse key also
+    # meets chunks without any of its records right after a boundary (`must` persists).
+    for seed in range(6):
+        recs = _sparse_trace(300 + seed, 12000, 6.0, share, 2, 12)
+        if algo == "tb":
+            _check("tb", recs, lambda: wm.TB(40, 20.0, 30000), 30000)
+        else:
+            _check("sw", recs, lambda: wm.SW(60, 2000), 2000)

@@ -15,7 +15,10 @@ engine's 2-B gathers and scattered stores are calibrated by tools/calib_fetch.sh
 (profiles/r04_calib). TCC_EA0_ATOMIC_sum (its own pass) is the L2's fabric-side atomic
 request count (north_star's atomic profile).
 
-usage: tools/pmc_json.py <profile dir> <config name> [--out profiles/pmc_summary.json]
+usage: tools/pmc_json.py <profile dir> <config name> [--out profiles/pmc_summary.json] [--tag DIR]
+
+The entry and _meta[config] always name the directory the values came from (--tag, else the
+profile directory as given): tests/test_pmc_provenance.py recomputes `step` from it.
 """
 import argparse
 import collections
@@ -54,28 +57,29 @@ def stage_of(name: str):
     return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("prof_dir")
-    ap.add_argument("config")
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
-        os.path.abspath(__file__))), "profiles", "pmc_summary.json"))
-    ap.add_argument("--tag", default="")
-    ap.add_argument("--batch", type=int, default=0,
-                    help="requests per GPU per step of the profiled run (default: the config's)")
-    ap.add_argument("--world", type=int, default=1, help="ranks of the profiled run")
-    a = ap.parse_args()
-    base = a.prof_dir.rstrip("/")
+def _csv(base, f, name):
+    """A pass's CSV in a tools/profile.sh output directory (gpurun_out/prof_<tag>/<f>/) or in
+    its committed copy (profiles/<tag>/, flattened)."""
+    for p in (f"{base}/{f}/{name}", f"{base}/{name}"):
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def summarize(base):
+    """Per-stage kernel-trace averages and PMC means of one profile directory, plus the
+    whole step's bytes (the entry bench.py reads as roofline.traffic)."""
+    base = base.rstrip("/")
     st = {}
-    for r in csv.DictReader(open(f"{base}/trace/trace_kernel_stats.csv")):
+    for r in csv.DictReader(open(_csv(base, "trace", "trace_kernel_stats.csv"))):
         s = stage_of(r["Name"])
         if s:
             st[s] = {"kernel": r["Name"], "calls": int(r["Calls"]),
                      "avg_us": float(r["AverageNs"]) / 1e3}
     counters = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in ("fetch", "write", "tcc", "sq", "atomic"):
-        p = f"{base}/{f}/{f}_counter_collection.csv"
-        if not os.path.exists(p):
+        p = _csv(base, f, f"{f}_counter_collection.csv")
+        if p is None:
             continue
         for r in csv.DictReader(open(p)):
             s = stage_of(r["Kernel_Name"])
@@ -105,8 +109,8 @@ def main():
     steps = st.get("unpermute", {}).get("calls")
     tot = collections.defaultdict(float)
     for f, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        p = f"{base}/{f}/{f}_counter_collection.csv"
-        if not os.path.exists(p):
+        p = _csv(base, f, f"{f}_counter_collection.csv")
+        if p is None:
             continue
         for r in csv.DictReader(open(p)):
             if "k_synth" not in r["Kernel_Name"] and r["Counter_Name"] == ctr:
@@ -115,6 +119,25 @@ def main():
         st["step"] = {"fetch_bytes": tot["FETCH_SIZE"] * 1024 * 2 / steps,
                       "write_bytes": tot["WRITE_SIZE"] * 1024 / steps, "steps": steps}
         st["step"]["hbm_bytes_per_launch"] = st["step"]["fetch_bytes"] + st["step"]["write_bytes"]
+    return st
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir")
+    ap.add_argument("config")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "profiles", "pmc_summary.json"))
+    ap.add_argument("--tag", default="",
+                    help="the directory the values are cited from (default: prof_dir as given, "
+                         "e.g. profiles/r06_sw_zipf); always recorded in _meta and the entry")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="requests per GPU per step of the profiled run (default: the config's)")
+    ap.add_argument("--world", type=int, default=1, help="ranks of the profiled run")
+    a = ap.parse_args()
+    st = summarize(a.prof_dir)
+    tag = a.tag or a.prof_dir.rstrip("/")
+    st["source"] = tag
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     # bench.py reports `roofline.traffic` only for the workload the profile was taken on
     st["batch"] = a.batch or DEFAULT_BATCH[a.config]
@@ -124,8 +147,7 @@ def main():
         "per-launch means; fetch_bytes = FETCH_SIZE KiB x1024 x2 (gfx950 wide-read "
         "correction), write_bytes = WRITE_SIZE KiB x1024; L2->fabric bytes, Infinity-Cache "
         "hits included (upper bound on HBM bytes)")
-    if a.tag:
-        out["_meta"][a.config] = a.tag
+    out["_meta"][a.config] = tag                    # provenance: where the values came from
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
     for s, d in sorted(st.items()):

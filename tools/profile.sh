@@ -2,7 +2,10 @@
 # Profile the bench workload with rocprofv3 on the GPU box (run from the repo root):
 #   kernel trace + stats, then one PMC pass per counter group (never combined with
 #   tracing domains; each pass bounded by its own timeout).
-# usage: tools/profile.sh <tag> [bench args...]
+# usage: tools/profile.sh <tag> [bench args...]     (tag e.g. r06_sw_zipf)
+# Then, back in the build container: tools/commit_profile.sh <tag> <config> copies the CSVs
+# to profiles/<tag>/ and folds them into profiles/pmc_summary.json with --tag profiles/<tag>
+# (the directory bench.py's roofline.traffic_source cites).
 set -o pipefail
 TAG=${1:-r01}; shift
 ARGS=${@:---steps 3 --warmup 1 --no-cpu-baseline}

@@ -100,28 +100,37 @@ class TB:
 
 # ---------------------------------------------------------------- the walk
 def walk(recs, st0, algo, w, stats):
-    """recs: [(t, p, op)] of one key in arrival order (times non-decreasing). Returns the
-    results [(allowed, remaining)] the walk + fill produce."""
+    """recs: [(t, p, op[, mine])] in arrival order — the walked key's records (mine, the
+    default) among other keys' records (mine False: they only take their place in the
+    region's 64-record chunks, as on the device). The key's times are non-decreasing.
+    Returns the results [(allowed, remaining)] the walk + fill produce for the key's records
+    (None for the others)."""
+    recs = [r if len(r) == 4 else (r[0], r[1], r[2], True) for r in recs]
     n = len(recs)
     nch = (n + 63) // 64
-    lo, hi = recs[0][0], recs[-1][0]
+    lo, hi = min(r[0] for r in recs), max(r[0] for r in recs)
     first1, first2 = {}, {}
-    for j, (t, p, op) in enumerate(recs):
-        if op == 0 and p == 1 and t not in first1:
+    for j, (t, p, op, mine) in enumerate(recs):
+        if mine and op == 0 and p == 1 and t not in first1:
             first1[t] = j
-        if op == 0 and p <= 2 and t not in first2:
+        if mine and op == 0 and p <= 2 and t not in first2:
             first2[t] = j
-    special = [any(r[2] != 0 for r in recs[c * 64:(c + 1) * 64]) for c in range(nch)]
-    mxs = [max((r[0] for r in recs[c * 64:(c + 1) * 64] if r[2] == 0), default=None) for c in range(nch)]
+    special = [any(r[3] and r[2] != 0 for r in recs[c * 64:(c + 1) * 64]) for c in range(nch)]
+    mxs = [max((r[0] for r in recs[c * 64:(c + 1) * 64] if r[3] and r[2] == 0), default=None)
+           for c in range(nch)]
     res = [None] * n
     verdict = {}                               # chunk -> (state copy, allow offsets)
     S = st0
 
     def detail(c, S):
         for j in range(c * 64, min(n, c * 64 + 64)):
-            t, p, op = recs[j]
-            res[j] = S.step(t, p, op)
+            t, p, op, mine = recs[j]
+            if mine:
+                res[j] = S.step(t, p, op)
         stats["detail"] += 1
+
+    def plain_before(c):                       # the key's last plain acquire before chunk c
+        return next((mxs[k] for k in range(c - 1, -1, -1) if mxs[k] is not None), None)
 
     def thresholds(S, W, C):                   # SW: T1(C), T2(C) in window W (thr_build)
         s = S.copy()
@@ -143,23 +152,32 @@ def walk(recs, st0, algo, w, stats):
     def rem0(c, tq1):                          # every acquire of chunk c is denied with remaining 0
         return mxs[c] is not None and (tq1 is None or mxs[c] < tq1)
 
-    cc, po, ts, must = 0, [], lo, False
-    K = S.copy()
+    st = dict(cc=0, po=[], ts=lo, must=False, mlast=None, K=S.copy())
+
+    def detail_at(c):                          # rl_hot.hpp walk: detail_at
+        detail(c, S)
+        if mxs[c] is not None:
+            st["mlast"] = mxs[c]
+        elif special[c]:
+            st["mlast"] = plain_before(c)
+        ml = st["mlast"]
+        if special[c]:                         # a reset may grant more: search again
+            st["ts"] = lo if ml is None else ml + 1
+        elif ml is not None:
+            st["ts"] = max(st["ts"], ml + 1)
+        st["must"] = ml is not None and S.pred(ml, 1)
+        st["cc"], st["K"], st["po"] = c + 1, S.copy(), []
+
     guard = 0
     while True:
         guard += 1
         assert guard < 10 * (nch + (hi - lo) + 100), "walk does not end"
+        cc, po, ts = st["cc"], st["po"], st["ts"]
         if cc >= nch:
             break
-        if not po and (must or special[cc]):
-            must = False
-            detail(cc, S)
-            if mxs[cc] is not None:
-                ts = max(ts, mxs[cc] + 1)
-                must = S.pred(mxs[cc], 1)
-            cc += 1
-            K = S.copy()
-            po = []
+        if not po and (st["must"] or special[cc]):
+            st["must"] = False
+            detail_at(cc)
             continue
         tf = None
         tq1 = None                             # the first ms >= ts the state grants (q >= 1)
@@ -186,56 +204,47 @@ def walk(recs, st0, algo, w, stats):
             if tf is not None:
                 break
             ts = lim + 1
+        st["ts"] = ts
         cs = nch - 1 if tf is None else rf // 64
         sp = next((c for c in range(cc + 1, cs + 1) if special[c]), None)
         if sp is not None:
-            verdict[cc] = (K.copy(), list(po), False)
+            verdict[cc] = (st["K"].copy(), list(po), False)
             for c in range(cc + 1, sp):
                 verdict[c] = (S.copy(), [], rem0(c, tq1))
-            detail(sp, S)
-            if mxs[sp] is not None:
-                ts = max(ts, mxs[sp] + 1)
-                must = S.pred(mxs[sp], 1)
-            cc, K, po = sp + 1, S.copy(), []
+            detail_at(sp)
             continue
         if tf is None:
-            verdict[cc] = (K.copy(), list(po), False)
+            verdict[cc] = (st["K"].copy(), list(po), False)
             for c in range(cc + 1, nch):
                 verdict[c] = (S.copy(), [], rem0(c, tq1))
             break
         if cs == cc and len(po) == 4:            # a fifth allow in the cursor chunk
             stats["conflict"] += 1
-            S = K.copy()
-            detail(cc, S)
-            if mxs[cc] is not None:
-                ts = max(ts, mxs[cc] + 1)
-                must = S.pred(mxs[cc], 1)
-            cc, K, po = cc + 1, S.copy(), []
+            S = st["K"].copy()
+            detail_at(cc)
             continue
         assert cs >= cc, ("allow before the cursor", cs, cc)
         if cs > cc:
-            verdict[cc] = (K.copy(), list(po), False)
+            verdict[cc] = (st["K"].copy(), list(po), False)
             for c in range(cc + 1, cs):
                 verdict[c] = (S.copy(), [], rem0(c, tq1))
-            cc, K, po = cs, S.copy(), []
-        po.append(rf % 64)
+            st["cc"], st["K"], st["po"] = cs, S.copy(), []
+        st["po"].append(rf % 64)
         a, _ = S.step(tf, pf)
         assert a == 1, "walk allow denied by the exact step"
         stats["allows"] += 1
-        ts = tf + 1
+        st["ts"] = tf + 1
         if S.pred(tf, 1):
             stats["burst"] += 1
-            S = K.copy()
-            detail(cc, S)
-            if mxs[cc] is not None:
-                ts = max(ts, mxs[cc] + 1)
-                must = S.pred(mxs[cc], 1)
-            cc, K, po = cc + 1, S.copy(), []
+            S = st["K"].copy()
+            detail_at(st["cc"])
     # fill: the verdict chunks
     for c, (Sv, o, z) in verdict.items():
         s = Sv.copy()
         for j in range(c * 64, min(n, c * 64 + 64)):
-            t, p, op = recs[j]
+            t, p, op, mine = recs[j]
+            if not mine:
+                continue
             assert op == 0
             if j - c * 64 in o:
                 res[j] = s.step(t, p)
