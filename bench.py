@@ -92,14 +92,15 @@ KEY_BYTES = 32 + 32            # state slot read + written
 # per-kernel bandwidth fractions; the headline roofline is the whole step's ALGORITHMIC
 # bytes over the whole step's time. Pass 1 of a routed two-pass batch
 # partitions only the n_normal records that pass 0 did not route to their final place
-# (DESIGN.md §4 "Hot-region routing"), so its kernels are charged for those alone.
+# (DESIGN.md §4 "Hot-region routing"), so k_group is charged for those alone.
 def kernel_io_bytes(name, n, u, n_lim, res_bytes, n_normal=None):
     lim = 2 if n_lim > 1 else 0
     nn = n if n_normal is None else n_normal
     return {
         "upsweep0": n * (8 + lim),
         "scatter0": n * (REQ_IN + lim + 16 + 4),          # request in; record 16 + position 4 out
-        "upsweep1": nn * 16, "scatter1": nn * (16 + 16 + 4),
+        # k_group: the normal records read twice (count, place), written once + positions
+        "group": nn * (16 + 16 + 16 + 4),
         "region": n * (16 + res_bytes) + u * KEY_BYTES,   # records in, packed results out, slots
         "unpermute": n * (4 + res_bytes + REQ_OUT),        # positions + gathered results in, decisions out
     }.get(name)
@@ -457,10 +458,11 @@ def run(name, args, ws, rank, local, dev, rehearse, steps, warm, parity_tokens):
     value = ws * n * steps / elapsed
 
     kern = {k: v for k, v in stages.items() if k not in ("total", "region_offsets") and v > 0}
-    if kern.get("scatter1", 0.0) < 0.05 * kern.get("scatter0", 1.0):
-        # one partition pass: the pass-1 marks only bracket empty time
-        for k in ("upsweep1", "scan1", "scatter1"):
-            kern.pop(k, None)
+    # the pass-1 marks bracket empty time (one pass; two passes group per bin since round 6)
+    for k in ("scan1", "scatter1"):
+        kern.pop(k, None)
+    if kern.get("group", 0.0) < 0.01 * kern.get("scatter0", 1.0):
+        kern.pop("group", None)
     U = stats["distinct_keys"]
     req_bytes = REQ_IN + (2 if n_lim > 1 else 0) + REQ_OUT
     algo_bytes = n * req_bytes + U * KEY_BYTES            # per GPU per step

@@ -27,7 +27,9 @@ namespace {
 // sets is averaged when rl_stage_times is called (no host sync inside a batch).
 constexpr int kMarks = 12;   // marks 0..11 on the engine stream
 constexpr int kStages = 11;
-const char* kStageNames[kStages] = {"upsweep0", "scan0", "scatter0", "upsweep1", "scan1",
+// (two-pass batches: "group" is k_group; "scan1" / "scatter1" are empty since round 6, when
+// k_group replaced the global second pass)
+const char* kStageNames[kStages] = {"upsweep0", "scan0", "scatter0", "group", "scan1",
                                     "scatter1", "region_offsets", "region", "unpermute", "total",
                                     "hot_fill"};
 const int kStagePairs[kStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6},
@@ -71,6 +73,8 @@ struct BatchScratch {
     uint32_t* region_count = nullptr;       // [P padded]
     uint32_t* region_start = nullptr;
     size_t region_cap = 0;
+    uint32_t* gtile = nullptr;              // k_group*: tile_base, tile_bin, per-tile counts
+    size_t gtile_cap = 0;
     BatchCtl* d_ctl = nullptr;
     hipEvent_t parted = nullptr;            // pipeline: partition done (partition stream)
     hipEvent_t freed = nullptr;             // pipeline: last reader of the set done (engine stream)
@@ -119,12 +123,17 @@ struct rl_engine {
     bool route = true;                      // rl_tune("route")
     bool region_order = true;               // rl_tune("region_order"): largest regions dispatched first
     uint32_t order_prefix = 4096;           // rl_tune("order_prefix"): ... after this many of the smallest
+    uint32_t group_bits = 12;               // rl_tune("group_bits"): two-pass batches' pass-0
+                                            // high digit (2^12 bins + the routed ones)
     uint32_t* order = nullptr;              // [order_cap + 1]
     size_t order_cap = 0;
     uint32_t* order_meta = nullptr;         // [kOrderMeta]
-    uint32_t* route_list = nullptr;         // [kRouteSlots] table of region ids (kNone = empty)
-    uint32_t* route_start = nullptr;        // [kRouteSlots] this batch's routed bins
-    uint32_t* route_cnt = nullptr;          // [kRouteSlots]
+    // One table per scratch set: with RL_OPT_PIPELINE batch k+1's partition runs while batch
+    // k's region stage still reads its routed ranges and writes the next table, so batch k uses
+    // set k % 2's table, written by batch k - 2 (set 0 only without the option: batch k - 1).
+    uint32_t* route_list = nullptr;         // [2][kRouteWords] region ids (kNone = empty), dense indices
+    uint32_t* route_start = nullptr;        // [2][kRouteSlots] this batch's routed bins
+    uint32_t* route_cnt = nullptr;          // [2][kRouteSlots]
     uint32_t solo_threshold = 4096;         // rl_tune("solo_threshold"): records per cache-on SW
                                             // region for the single-key allow-run pass (0: off)
     uint32_t* solo_list = nullptr;          // [kSoloMax + 1]: the listed regions, then their count
@@ -304,12 +313,12 @@ extern "C" int rl_create(const rl_opts* opts, rl_engine** out) {
     if (rc == RL_OK) rc = dalloc(&e->d_lims, RL_MAX_LIMITERS);
     if (rc == RL_OK) rc = dalloc(&e->hot_list, kHotListWords);
     if (rc == RL_OK) rc = dalloc(&e->hot_info, kHotMax);
-    if (rc == RL_OK) rc = dalloc(&e->route_list, kRouteSlots);
-    if (rc == RL_OK) rc = dalloc(&e->route_start, kRouteSlots);
-    if (rc == RL_OK) rc = dalloc(&e->route_cnt, kRouteSlots);
+    if (rc == RL_OK) rc = dalloc(&e->route_list, 2 * kRouteWords);
+    if (rc == RL_OK) rc = dalloc(&e->route_start, 2 * kRouteSlots);
+    if (rc == RL_OK) rc = dalloc(&e->route_cnt, 2 * kRouteSlots);
     if (rc == RL_OK) rc = dalloc(&e->order_meta, kOrderMeta);
     if (rc == RL_OK) rc = dalloc(&e->solo_list, kSoloMax + 1);
-    if (rc == RL_OK && hipMemset(e->route_list, 0xFF, kRouteSlots * sizeof(uint32_t)) != hipSuccess)
+    if (rc == RL_OK && hipMemset(e->route_list, 0xFF, 2 * kRouteWords * sizeof(uint32_t)) != hipSuccess)
         rc = RL_E_DEVICE;
     if (rc != RL_OK) { rl_destroy(e); return rc; }
     std::memset(e->h_ctl, 0, sizeof(BatchCtl));
@@ -328,7 +337,7 @@ extern "C" void rl_destroy(rl_engine* e) {
         dfree(B.rec0); dfree(B.rec1); dfree(B.pos0); dfree(B.pos1); dfree(B.res); dfree(B.tok);
         dfree(B.ext); dfree(B.digit);
         dfree(B.counts); dfree(B.bin_total); dfree(B.bin_base);
-        dfree(B.region_count); dfree(B.region_start);
+        dfree(B.region_count); dfree(B.region_start); dfree(B.gtile);
         dfree(B.d_ctl);
         if (B.parted) (void)hipEventDestroy(B.parted);
         if (B.freed) (void)hipEventDestroy(B.freed);
@@ -485,7 +494,7 @@ static int grow_once(rl_engine* e, size_t li) {
     e->n_regions = base;
     ++e->grows;
     // region ids changed: the next batch routes nothing (its hot preparation lists anew)
-    HIP_OK(hipMemset(e->route_list, 0xFF, kRouteSlots * sizeof(uint32_t)));
+    HIP_OK(hipMemset(e->route_list, 0xFF, 2 * kRouteWords * sizeof(uint32_t)));
     return upload_limiters(e);
 }
 
@@ -547,7 +556,7 @@ static int ensure_scratch(rl_engine* e, BatchScratch& B, size_t n, bool wide, ui
     return RL_OK;
 }
 
-// rstart / rend per bin for two-pass partitions (k_bin_bounds).
+// rstart / rend per region for two-pass partitions (k_group).
 static int ensure_regions(BatchScratch& B, size_t bins) {
     if (bins <= B.region_cap) return RL_OK;
     dfree(B.region_count); dfree(B.region_start);
@@ -619,15 +628,18 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     const int bitsP = std::max(1, ceil_log2(n_bins));
     const int passes = bitsP <= kMaxDigitBits ? 1 : 2;
     if (bitsP > 2 * kMaxDigitBits) return RL_E_LIMITERS;
-    const int d0 = passes == 1 ? bitsP : bitsP - bitsP / 2;
-    const int d1 = bitsP - d0;
-    // hot-region routing: pass 0 gets kRouteSlots bins beyond the 2^d0 low-digit ones. The
+    // Two passes: pass 0 partitions by the high dh bits of the region id (2^dh bins of 2^s0
+    // consecutive regions), then k_group groups each bin by region locally (rl_partition.hip)
+    const int dh = passes == 1 ? bitsP
+                               : std::max(bitsP - kMaxDigitBits, std::min<int>((int)e->group_bits, kMaxDigitBits));
+    const int s0 = bitsP - dh;
+    // hot-region routing: pass 0 gets kRouteBins dense bins beyond the 2^dh high-digit ones. The
     // hot path is gated per limiter: regions of a limiter with the local cache are never
     // listed hot (k_hot_select), so they are never routed either; the other limiters keep it.
     const bool hot_on = e->hot_threshold > 0;
-    const bool route = hot_on && e->route && passes == 2 && !e->pipeline &&
-                       (1u << d0) + kRouteSlots <= (1u << kMaxDigitBits);
-    const uint32_t nb0 = route ? (1u << d0) + kRouteSlots : 1u << d0;
+    const bool route = hot_on && e->route && passes == 2 &&
+                       (1u << dh) + kRouteBins <= (1u << kMaxDigitBits);
+    const uint32_t nb0 = route ? (1u << dh) + kRouteBins : 1u << dh;
     // Scratch set and partition stream. With RL_OPT_PIPELINE the partition (stages 1-3)
     // runs on e->pstream into one of two scratch sets, so batch k+1's partition overlaps
     // batch k's region stage; the region stage and the unpermute stay on e->stream (state
@@ -636,15 +648,18 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     // enqueued on e->stream (inputs copied or produced there, or the caller's stream).
     const int set = e->pipeline ? e->next_set : 0;
     BatchScratch& B = e->sc[set];
+    uint32_t* r_list = e->route_list + (size_t)set * kRouteWords;
+    uint32_t* r_start = e->route_start + (size_t)set * kRouteSlots;
+    uint32_t* r_cnt = e->route_cnt + (size_t)set * kRouteSlots;
     hipStream_t ps = e->pipeline ? e->pstream : s;
-    const size_t need_counts = (size_t)std::max<uint32_t>(nb0, 1u << d1) * nt;
+    const size_t need_counts = (size_t)nb0 * nt;
     if (e->pipeline && (n > B.cap_n || (wide && !B.cap_wide) || need_counts > B.counts_cap ||
                         (passes == 2 && n_bins > B.region_cap))) {
         // growing a set frees its old buffers: nothing may still be using them
         HIP_OK(hipStreamSynchronize(s));
         HIP_OK(hipStreamSynchronize(ps));
     }
-    int rc = ensure_scratch(e, B, n, wide, std::max<uint32_t>(nb0, 1u << d1), nt);
+    int rc = ensure_scratch(e, B, n, wide, nb0, nt);
     if (rc != RL_OK) return rc;
     if (passes == 2) {
         rc = ensure_regions(B, n_bins);
@@ -687,13 +702,13 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = B.d_ctl;
     pa.counts = B.counts; pa.bin_base = B.bin_base; pa.ablate = e->ablate;
     pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu; pa.sc_split = e->sc_split;
-    // ---- pass 0 (low digit) from the caller's arrays; routed hot regions get bins
-    // 2^d0 + slot and their records go straight to the final array (rec1)
-    pa.digit_shift = 0; pa.digit_bits = route ? ceil_log2(nb0) : d0;
+    // ---- pass 0 (the high digit: region >> s0) from the caller's arrays; routed hot
+    // regions get bins 2^dh + slot and their records go straight to the final array (rec1)
+    pa.digit_shift = s0; pa.digit_bits = route ? ceil_log2(nb0) : dh;
     pa.n_bins_pass = nb0;
-    pa.rec_out = B.rec0; pa.pos_out = B.pos0;
+    pa.rec_out = passes == 2 ? B.rec0 : B.rec1; pa.pos_out = B.pos0;
     if (route) {
-        pa.route_list = e->route_list; pa.lo_bins = 1u << d0; pa.rec_out_route = B.rec1;
+        pa.route_list = r_list; pa.lo_bins = 1u << dh; pa.rec_out_route = B.rec1;
         pa.digit = B.digit;
     }
     HIP_OK(launch_upsweep(pa, true, wide, ps));
@@ -703,48 +718,45 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     mark_on(e, ps, 2);
     HIP_OK(launch_scatter(pa, true, wide, ps));
     if (route)
-        HIP_OK(launch_route_ranges(B.bin_base, B.bin_total, 1u << d0, e->route_start, e->route_cnt,
+        HIP_OK(launch_route_ranges(r_list, B.bin_base, B.bin_total, 1u << dh, r_start, r_cnt,
                                    B.d_ctl, ps));
     mark_on(e, ps, 3);
-    const void* rec_final = B.rec0;
+    const void* rec_final = B.rec1;
     const uint32_t* rstart = B.bin_base;
     const uint32_t* rcount = B.bin_total;
     const uint32_t* rend = nullptr;
     if (passes == 2) {
-        // ---- pass 1 (high digit) over the records; stable, so the final order is
-        // bin-major and arrival-ordered inside each bin.
-        pa.digit_shift = d0; pa.digit_bits = d1;
-        pa.n_bins_pass = 1u << d1;
-        pa.route_list = nullptr; pa.digit = nullptr;
-        pa.n_dev = route ? &B.d_ctl->n_normal : nullptr;  // routed records stay where pass 0 put them
-        pa.rec_in = B.rec0; pa.rec_out = B.rec1; pa.pos_out = B.pos1;
-        HIP_OK(launch_upsweep(pa, false, wide, ps));
-        mark_on(e, ps, 4);
-        HIP_OK(launch_scan_rows(B.counts, B.counts, 1u << d1, nt, B.bin_total, ps));
-        HIP_OK(launch_scan_small(B.bin_total, B.bin_base, 1u << d1, ps));
-        mark_on(e, ps, 5);
-        HIP_OK(launch_scatter(pa, false, wide, ps));
-        rec_final = B.rec1;
-    } else {
-        mark_on(e, ps, 4);
-        mark_on(e, ps, 5);
-    }
-    mark_on(e, ps, 6);
-    if (passes == 2) {
-        // bin boundaries of the final order: binary searches inside the high-digit runs
-        // that pass 1's scan delimits (no per-request atomics: a hot bin would serialise
-        // them; no full read of the records)
-        BoundsArgs ba{};
-        ba.rec = rec_final; ba.n = (uint32_t)n; ba.n_lim = (uint32_t)e->lims.size();
-        ba.lims = e->d_lims; ba.shard_bits = e->shard_bits;
-        ba.rstart = B.region_start; ba.rend = B.region_count;
-        ba.hi_base = B.bin_base; ba.hi_total = B.bin_total;
-        ba.n_bins = n_bins; ba.d0 = d0; ba.d1 = d1;
-        HIP_OK(launch_bin_bounds(ba, wide, ps));
+        // ---- each normal pass-0 bin grouped by region in its own range of the final array
+        // (stable: arrival order inside each region); the regions' bounds and the pass-0 ->
+        // final positions (pos1) come with it. Routed records stay where pass 0 put them.
+        GroupArgs ga{};
+        ga.rec_in = B.rec0; ga.rec_out = B.rec1; ga.pos_out = B.pos1;
+        ga.bin_base = B.bin_base; ga.bin_total = B.bin_total;
+        ga.rstart = B.region_start; ga.rend = B.region_count;
+        ga.lims = e->d_lims; ga.n_lim = (uint32_t)e->lims.size(); ga.shard_bits = e->shard_bits;
+        ga.n_bins0 = 1u << dh; ga.sub_bits = (uint32_t)s0; ga.n_regions = n_bins;
+        ga.tile_recs = group_tile_recs((uint32_t)s0);
+        ga.pad = (uint32_t)n;
+        ga.ablate = e->ablate;
+        ga.max_tiles = (uint32_t)((n + ga.tile_recs - 1) / ga.tile_recs) + ga.n_bins0;
+        const size_t words = (size_t)ga.n_bins0 + 1 + (size_t)ga.max_tiles * (1 + ((size_t)1 << s0));
+        if (words > B.gtile_cap) {
+            if (e->pipeline) { HIP_OK(hipStreamSynchronize(s)); HIP_OK(hipStreamSynchronize(ps)); }
+            dfree(B.gtile);
+            if (dalloc(&B.gtile, words) != RL_OK) { B.gtile_cap = 0; return RL_E_NOMEM; }
+            B.gtile_cap = words;
+        }
+        ga.tile_base = B.gtile;
+        ga.tile_bin = B.gtile + ga.n_bins0 + 1;
+        ga.tcount = ga.tile_bin + ga.max_tiles;
+        HIP_OK(launch_group(ga, wide, ps));
         rstart = B.region_start;
         rcount = nullptr;
         rend = B.region_count;
     }
+    mark_on(e, ps, 4);
+    mark_on(e, ps, 5);
+    mark_on(e, ps, 6);
     if (e->pipeline) {
         HIP_OK(hipEventRecord(B.parted, ps));
         HIP_OK(hipStreamWaitEvent(s, B.parted, 0));
@@ -778,7 +790,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     if (hot) {
         uint32_t* hot_count = e->hot_list + kHotMax;
         HIP_OK(hipMemsetAsync(hot_count, 0, kHotMetaWords * sizeof(uint32_t), s));
-        if (route) HIP_OK(launch_hot_route_list(e->route_list, e->route_cnt, e->hot_list, hot_count, s));
+        if (route) HIP_OK(launch_hot_route_list(r_list, r_cnt, e->hot_list, hot_count, s));
         HIP_OK(launch_hot_select(rstart, rcount, rend, n_bins, hot_thr, e->hot_list,
                                  hot_count, e->hot_mark, e->epoch, cache ? e->d_lims : nullptr,
                                  e->d_region_lim, s));
@@ -786,7 +798,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ra.epoch = e->epoch;
         ra.hot_info = e->hot_info; ra.hot_summ = e->hot_summ;
         ra.hot_summ2 = e->hot_summ + e->hot_summ_l1 * 8; ra.hot_total = e->hot_list + kHotMax + kHotTotalOff;
-        ra.route_list = e->route_list; ra.route_start = e->route_start; ra.route_cnt = e->route_cnt;
+        ra.route_list = r_list; ra.route_start = r_start; ra.route_cnt = r_cnt;
         ra.walk_tab = e->walk ? e->walk_tab : nullptr;
         ra.walk_min = e->walk_min;
         HIP_OK(launch_hot_prepare(ra, wide, s));          // dominant keys, chunk summaries
@@ -821,8 +833,8 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     mark(e, 10);
     // (hot: the fill ran on the side stream, joined by launch_region)
     // the next batch's routed regions: this batch's largest hot regions (two-pass tables)
-    if (hot && e->route && passes == 2 && !e->pipeline)
-        HIP_OK(launch_route_next(e->hot_info, e->hot_list + kHotMax, hot_thr, e->route_list, s));
+    if (hot && e->route && passes == 2)
+        HIP_OK(launch_route_next(e->hot_info, e->hot_list + kHotMax, hot_thr, r_list, s));
     HIP_OK(launch_stats_reduce(e->d_stats, B.d_ctl, s));
     mark(e, 11);
     mark(e, 8);
@@ -1168,6 +1180,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
         e->route = value != 0;
         return RL_OK;
     }
+    if (std::strcmp(key, "group_bits") == 0) {        // two-pass batches: pass-0 high-digit bits
+        if (value < 1 || value > kMaxDigitBits) return RL_E_INVALID_ARG;
+        e->group_bits = (uint32_t)value;
+        return RL_OK;
+    }
     if (std::strcmp(key, "walk") == 0) {              // allow walks of the hot chains
         e->walk = value != 0;
         if (!e->walk && e->walk_tab) {                 // (hipFree waits for the batches in flight)
@@ -1497,6 +1514,13 @@ extern "C" int rl_debug_fetch(rl_engine* e, const char* what, void* out, size_t 
         const size_t nb = std::min(bytes, e->dbg_cap * sizeof(uint64_t));
         HIP_OK(hipMemcpy(out, e->dbg, nb, hipMemcpyDeviceToHost));
         return (int)(nb / (kDbgWords * sizeof(uint64_t)));
+    }
+    if (std::strcmp(what, "bin_totals") == 0) {      // the last batch's pass-0 bin sizes
+        const BatchScratch& B = e->sc[e->pipeline ? e->next_set ^ 1 : 0];
+        HIP_OK(hipStreamSynchronize(e->stream));
+        const size_t nb = std::min(bytes, ((size_t)1 << kMaxDigitBits) * sizeof(uint32_t));
+        HIP_OK(hipMemcpy(out, B.bin_total, nb, hipMemcpyDeviceToHost));
+        return (int)(nb / sizeof(uint32_t));
     }
     return RL_E_INVALID_ARG;
 }

@@ -158,6 +158,14 @@ __global__ __launch_bounds__(1024) void k_route_next(const HotInfo* __restrict__
         __syncthreads();
         if (s_placed >= kRouteMax) break;              // (block-uniform)
     }
+    __syncthreads();
+    // the slots' dense indices (pass-0 bin lo_bins + idx): occupied slots before each slot
+    __shared__ uint32_t s_tmp[16];
+    static_assert(kRouteSlots == 2 * 1024, "two slots per thread");
+    const uint32_t occ = (s_tab[2 * t] != kNone ? 1u : 0u) + (s_tab[2 * t + 1] != kNone ? 1u : 0u);
+    const uint32_t ex = block_exclusive_scan<1024>(occ, s_tmp, nullptr);
+    route_list[kRouteSlots + 2 * t] = ex;
+    route_list[kRouteSlots + 2 * t + 1] = ex + (s_tab[2 * t] != kNone ? 1u : 0u);
     for (uint32_t i = t; i < kRouteSlots; i += blockDim.x) route_list[i] = s_tab[i];
 }
 

@@ -12,7 +12,8 @@
 //   2. k_scan_rows/k_scan_small : exclusive scan of the [bin][tile] histogram.
 //   3. k_scatter  : stable partition (wave ballot-match ranking) of the requests
 //                   into bin order, packed into 16-byte records.
-//   (1-3 repeat once more when a limiter set has > 1024 bins.)
+//   (more than 8192 regions: pass 0 partitions by the region's high digit and k_group
+//    then groups each pass-0 bin by region locally.)
 //   4. k_regions  : one single-wave workgroup per REGION. The wave loads its region's
 //                   256 state slots (8 KB) into LDS once (or faults in single buckets of
 //                   a sparse region), streams the region's records in arrival order and
@@ -213,9 +214,13 @@ __device__ inline uint32_t bin_of(const PartArgs& a, uint32_t i, const LimLds& L
 // routed iff it sits at one of its two slots (route_slots), and that slot is its bin.
 struct RouteLds {
     uint32_t key[kRouteSlots];
+    uint16_t idx[kRouteSlots];               // dense routed bin of the slot (lo_bins + idx)
 };
 __device__ inline void route_load(RouteLds& R, const uint32_t* table) {
-    for (uint32_t s = threadIdx.x; s < kRouteSlots; s += blockDim.x) R.key[s] = table[s];
+    for (uint32_t s = threadIdx.x; s < kRouteSlots; s += blockDim.x) {
+        R.key[s] = table[s];
+        R.idx[s] = (uint16_t)table[kRouteSlots + s];
+    }
     __syncthreads();
 }
 __device__ inline uint32_t route_find(const RouteLds& R, uint32_t b) {
@@ -224,12 +229,13 @@ __device__ inline uint32_t route_find(const RouteLds& R, uint32_t b) {
     const uint32_t k1 = R.key[s1], k2 = R.key[s2];         // independent reads
     return k1 == b ? s1 : k2 == b ? s2 : kNone;
 }
-// Partition digit of global bin g in this pass: routed region -> lo_bins + slot, else
-// the low digit (pass 0 with routing); otherwise the digit at digit_shift.
+// Partition digit of global bin g (a region id) in pass 0: routed region -> lo_bins + its dense index,
+// else its high digit g >> digit_shift (two-pass batches: k_group then groups each of
+// those bins by region; one-pass batches: digit_shift 0, the region itself).
 __device__ inline uint32_t pass_digit(const PartArgs& a, uint32_t g, const RouteLds& R) {
     if (a.route_list) {
         const uint32_t rs = route_find(R, g);
-        return rs != kNone ? a.lo_bins + rs : (g & (a.lo_bins - 1));
+        return rs != kNone ? a.lo_bins + R.idx[rs] : (g >> a.digit_shift);
     }
     return (g >> a.digit_shift) & ((1u << a.digit_bits) - 1);
 }

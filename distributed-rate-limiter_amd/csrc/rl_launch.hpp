@@ -16,6 +16,7 @@ enum : uint32_t {
     kAblNoMatch = 1u << 2,       // scatter: skip the ballot match (rank 0 for every lane)
     kAblNoPosStore = 1u << 3,    // scatter: skip pos_out
     kAblNoBarrier = 1u << 4,     // scatter: skip the two per-round barriers
+    kAblGroupSeq = 1u << 5,      // k_gplace: store records at their pass-0 index (coalesced)
     kAblNoStep = 1u << 8,        // region: skip the per-request semantics
     kAblNoProbe = 1u << 9,       // region: slot = home (no lookup / insert)
     kAblNoRounds = 1u << 10,     // region: one round, no peer match
@@ -83,8 +84,8 @@ struct PartArgs {
     uint32_t n_bins_pass;      // bins of this pass (0: 1 << digit_bits)
     // Hot-region routing (pass 0 of a two-pass batch): route_list is a kRouteSlots-entry
     // table of region ids (kNone = empty; the previous batch's largest hot regions, each at
-    // one of its two hash slots, route_slots). A routed region's requests get bin
-    // lo_bins + slot, every other request its low digit; the upsweep stores each request's
+    // one of its two hash slots, route_slots) followed by the slots' dense indices. A routed
+    // region's requests get bin lo_bins + idx[slot], every other request its high digit; the upsweep stores each request's
     // digit in `digit`, the scatter reads it back, and routed records go straight to
     // rec_out_route (the final record array) at their pass-0 position, skipping pass 1.
     const uint32_t* route_list;
@@ -190,6 +191,13 @@ constexpr uint32_t kHotRoutedBit = 0x80000000u;
 // sits at one of its two hash slots (route_slots): a lookup is two independent reads.
 constexpr uint32_t kRouteMax = 512;
 constexpr uint32_t kRouteSlots = 2048;
+// Routed regions get DENSE pass-0 bins: slot s's region goes to bin lo_bins + idx[s] (idx =
+// the number of occupied slots before s, written by k_route_next after the ids, at
+// route_list + kRouteSlots), so pass 0 has 2^dh + kRouteBins bins instead of 2^dh + the
+// 2048 slots (k_route_next places at most kRouteMax + 127 regions).
+constexpr uint32_t kRouteBins = 1024;
+static_assert(kRouteMax + 128 <= kRouteBins, "k_route_next places up to kRouteMax + 127");
+constexpr uint32_t kRouteWords = 2 * kRouteSlots;   // a route table: ids, then dense indices
 __host__ __device__ inline void route_slots(uint32_t region, uint32_t& s1, uint32_t& s2) {
     s1 = (region * 0x9E3779B1u) >> 21;
     s2 = ((region ^ 0x5BD1E995u) * 0x85EBCA6Bu) >> 21;
@@ -217,20 +225,37 @@ struct HotInfo {             // one listed hot region
     uint64_t tag2;           // a second dominant key (ok bit 1): its own chain wave
 };
 
-struct BoundsArgs {
-    const void* rec;           // records in final (bin) order
-    uint32_t n;
-    uint32_t n_lim;
+// Two-pass batches, after pass 0 (which partitions by the high digit of the region id):
+// k_gtiles / k_gcount / k_gscan / k_gplace group each normal pass-0 bin's records by region
+// inside the bin's own range of the final record array (rstart / rend per region, pos_out
+// per pass-0 position). A bin is cut into tiles of tile_recs records, one wave each.
+struct GroupArgs {
+    const void* rec_in;        // pass-0 records (bin-major, arrival order inside each bin)
+    void* rec_out;             // the final record array (region-major)
+    uint32_t* pos_out;         // [n_normal]: final position of pass-0 position j
+    const uint32_t* bin_base;  // [n_bins0] pass-0 scan: first record of each normal bin
+    const uint32_t* bin_total; // [n_bins0]
+    uint32_t* rstart;          // [n_regions] first record of each region (final order)
+    uint32_t* rend;            // [n_regions]
     const DevLimiter* lims;
+    uint32_t n_lim;
     int32_t shard_bits;
-    uint32_t* rstart;          // [n_bins]
-    uint32_t* rend;            // [n_bins]
-    const uint32_t* hi_base;   // [2^d1] first record of each high-digit run (pass-1 scan)
-    const uint32_t* hi_total;  // [2^d1] records in each high-digit run
-    uint32_t n_bins;
-    int32_t d0;                // low-digit bits (pass 0)
-    int32_t d1;                // high-digit bits (pass 1)
+    uint32_t n_bins0;          // normal pass-0 bins (2^dh)
+    uint32_t sub_bits;         // s0: regions per pass-0 bin = 2^s0 (region id = bin << s0 | sub)
+    uint32_t n_regions;
+    uint32_t tile_recs;        // records per tile (one wave counts, then places, a tile)
+    uint32_t max_tiles;        // tiles the scratch holds (ceil(n / tile_recs) + n_bins0)
+    uint32_t* tile_base;       // [n_bins0 + 1] first tile of each bin; [n_bins0] = tiles
+    uint32_t* tile_bin;        // [max_tiles] bin of each tile
+    uint32_t* tcount;          // [max_tiles][2^s0] per-tile region counts, then cursors
+    uint32_t pad;              // the batch size: rec_out / pos_out hold 64 padding entries past it
+    uint32_t ablate;           // rl_tune("ablate") (measurement only)
 };
+// records per tile of the grouping: 8192, or 32 per region of a bin when bins are wide
+__host__ __device__ inline uint32_t group_tile_recs(uint32_t sub_bits) {
+    const uint32_t t = 32u << sub_bits;
+    return t > 8192u ? t : 8192u;
+}
 
 struct UnpermArgs {
     const uint32_t* pos0;
@@ -344,12 +369,13 @@ hipError_t launch_hot_select(const uint32_t* rstart, const uint32_t* rcount, con
                              uint32_t n_bins, uint32_t threshold, uint32_t* hot_list,
                              uint32_t* hot_count, uint32_t* hot_mark, uint32_t epoch,
                              const DevLimiter* lims, const uint8_t* region_lim, hipStream_t s);
-hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s);
+hipError_t launch_group(const GroupArgs& a, bool wide, hipStream_t s);
 // Routing: after the pass-0 scan, copy the routed bins' ranges (before pass 1 reuses the scan
 // arrays) and set ctl->n_normal; after the hot selection, list the routed regions first; after
 // the batch's hot preparation, the next batch's route list (largest listed regions >= thr).
-hipError_t launch_route_ranges(const uint32_t* bin_base, const uint32_t* bin_total, uint32_t lo_bins,
-                               uint32_t* route_start, uint32_t* route_cnt, BatchCtl* ctl, hipStream_t s);
+hipError_t launch_route_ranges(const uint32_t* route_list, const uint32_t* bin_base,
+                               const uint32_t* bin_total, uint32_t lo_bins, uint32_t* route_start,
+                               uint32_t* route_cnt, BatchCtl* ctl, hipStream_t s);
 hipError_t launch_hot_route_list(const uint32_t* route_list, const uint32_t* route_cnt,
                                  uint32_t* hot_list, uint32_t* hot_meta, hipStream_t s);
 // Normal-region dispatch order, largest power-of-two size class first (regions are

@@ -480,47 +480,320 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
     }
 }
 
-// Bin boundaries of the final record order (two-pass partitions): rstart[b] / rend[b]
-// for every bin b < n_bins. The high-digit pass leaves run hi = [hi_base[hi],
-// hi_base[hi] + hi_total[hi]) whose records are still in low-digit order (the pass is
-// stable over the low-digit pass's output), so each low digit's first record is a
-// binary search inside its run: one workgroup per run, ~log2(run) record probes per
-// bin instead of reading every record of the batch.
+// ------------------------------------------------------------------ 3g. local grouping
+// Two-pass batches. Pass 0 partitions by the HIGH dh bits of the region id (bin = region >>
+// s0; routed hot regions to bins of their own), so a normal pass-0 bin holds the records of
+// 2^s0 consecutive regions in arrival order. The bins are then grouped by region inside their
+// own ranges of the final array. A bin is cut into tiles of group_tile_recs records (8192):
+//   k_gtiles  tiles per bin (scan) and each tile's bin;
+//   k_gcount  one wave per tile: its records per region (wave-private LDS counters);
+//   k_gscan   one workgroup per bin: per region, the prefix over the bin's tiles, then the
+//             regions' starts (region-major, then tile: stable) -> each tile's cursors and
+//             the regions' bounds (rstart / rend: the old k_bin_bounds searches are gone);
+//   k_gplace  one wave per tile: rank inside each 64-record round by ballot match, place at
+//             the tile's own cursors (no barrier), pos_out[j] = final position.
+// A tile's output lands in the bin's window (a few hundred KB) within microseconds, so the
+// scattered 16-B record stores complete their sectors while the lines are still in L2 (the
+// global second pass spread every bin's runs over the whole batch and left half-written
+// sectors: write amplification 1.57x). Tiles rather than one workgroup per bin: the largest
+// bins hold ~8x the mean (sw_zipf: 230K records against 30K), and one workgroup per bin made
+// the largest set the stage (2.0 ms). pos_out keeps the unpermute's two gathers local.
+constexpr int kGroupThreads = 256;
+constexpr int kGroupWaves = kGroupThreads / 64;
+constexpr int kGroupDepth = 8;                       // rounds of records in flight per wave
+
+__global__ __launch_bounds__(1024) void k_gtiles(GroupArgs a) {
+    __shared__ uint32_t tmp[16];
+    const uint32_t t = threadIdx.x, nb = a.n_bins0, T = a.tile_recs;
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t b0 = min(t * per, nb), b1 = min(b0 + per, nb);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += (a.bin_total[b] + T - 1) / T;
+    uint32_t tot;
+    uint32_t base = block_exclusive_scan<1024>(sum, tmp, &tot);
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t nt = (a.bin_total[b] + T - 1) / T;
+        a.tile_base[b] = base;
+        for (uint32_t j = 0; j < nt && base + j < a.max_tiles; ++j) a.tile_bin[base + j] = b;
+        base += nt;
+    }
+    if (t == 0) a.tile_base[nb] = min(tot, a.max_tiles);
+}
+
+// (tile t of the batch: bin, first record, end)
+__device__ inline void group_tile(const GroupArgs& a, uint32_t t, uint32_t& b, uint32_t& beg,
+                                  uint32_t& end) {
+    b = a.tile_bin[t];
+    const uint32_t j = t - a.tile_base[b];
+    const uint32_t bb = a.bin_base[b], be = bb + a.bin_total[b];
+    beg = bb + j * a.tile_recs;
+    end = min(beg + a.tile_recs, be);
+}
+
 template <class Codec>
-__global__ __launch_bounds__(256) void k_bin_bounds(BoundsArgs a) {
-    __shared__ uint32_t s_base[256];
-    __shared__ uint8_t s_bits[256];
-    __shared__ uint32_t s_lb[(1u << kMaxDigitBits) + 1];
-    for (uint32_t l = threadIdx.x; l < a.n_lim; l += 256) {
-        s_base[l] = a.lims[l].region_base;
-        s_bits[l] = (uint8_t)a.lims[l].region_bits;
-    }
-    __syncthreads();
-    const typename Codec::Rec* recs = (const typename Codec::Rec*)a.rec;
-    const uint32_t nlo = 1u << a.d0, lo_mask = nlo - 1;
-    auto lo_of = [&](uint32_t i) {
-        const typename Codec::Rec r = recs[i];
-        const uint32_t lim = Codec::limiter_of(r);
-        return (s_base[lim] + region_local(r.h, a.shard_bits, s_bits[lim])) & lo_mask;
-    };
-    const uint32_t hi = blockIdx.x;
-    const uint32_t beg = a.hi_base[hi], end = beg + a.hi_total[hi];
-    for (uint32_t lo = threadIdx.x; lo <= nlo; lo += 256) {
-        uint32_t L = beg, R = end;                    // first record with low digit >= lo
-        if (lo == nlo) L = end;
-        while (L < R) {
-            const uint32_t m = L + (R - L) / 2;
-            if (lo_of(m) < lo) L = m + 1;
-            else R = m;
+struct GroupSub {                                    // a record's region inside its bin
+    uint32_t base[256];
+    uint8_t bits[256];
+    __device__ inline void load(const GroupArgs& a) {
+        for (uint32_t l = threadIdx.x; l < a.n_lim; l += blockDim.x) {
+            base[l] = a.lims[l].region_base;
+            bits[l] = (uint8_t)a.lims[l].region_bits;
         }
-        s_lb[lo] = L;
+    }
+    __device__ inline uint32_t of(const GroupArgs& a, const typename Codec::Rec& r, uint32_t smask) const {
+        const uint32_t lim = Codec::limiter_of(r);
+        return (base[lim] + region_local(r.h, a.shard_bits, bits[lim])) & smask;
+    }
+};
+
+template <class Codec>
+__global__ __launch_bounds__(kGroupThreads) void k_gcount(GroupArgs a) {
+    using Rec = typename Codec::Rec;
+    extern __shared__ uint32_t gl[];                 // [waves][2^s0]
+    __shared__ GroupSub<Codec> G;
+    G.load(a);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t nsub = 1u << a.sub_bits, smask = nsub - 1u;
+    uint32_t* cw = gl + wid * nsub;
+    const Rec* __restrict__ in = (const Rec*)a.rec_in;
+    const uint32_t n_t = a.tile_base[a.n_bins0];
+    for (uint32_t t = blockIdx.x * kGroupWaves + wid; t < n_t; t += gridDim.x * kGroupWaves) {
+        uint32_t b, beg, end;
+        group_tile(a, t, b, beg, end);
+        for (uint32_t k = lane; k < nsub; k += 64) cw[k] = 0;
+        wave_fence();
+        for (uint32_t i0 = beg; i0 < end; i0 += 64 * kGroupDepth) {
+            Rec r[kGroupDepth];
+#pragma unroll
+            for (int k = 0; k < kGroupDepth; ++k) {
+                const uint32_t i = i0 + (uint32_t)k * 64 + lane;
+                r[k] = ld_rec<kNtRgRec>(in + (i < end ? i : end - 1));
+            }
+#pragma unroll
+            for (int k = 0; k < kGroupDepth; ++k)
+                if (i0 + (uint32_t)k * 64 + lane < end) atomicAdd(&cw[G.of(a, r[k], smask)], 1u);
+        }
+        wave_fence();
+        uint32_t* dst = a.tcount + (size_t)t * nsub;
+        for (uint32_t k = lane; k < nsub; k += 64) dst[k] = cw[k];
+        wave_fence();
+    }
+}
+
+__global__ __launch_bounds__(kGroupThreads) void k_gscan(GroupArgs a) {
+    extern __shared__ uint32_t tot[];                // [2^s0] the regions' record counts
+    __shared__ uint32_t tmp[kGroupWaves];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t nsub = 1u << a.sub_bits;
+    const uint32_t t0 = a.tile_base[b], t1 = a.tile_base[b + 1 <= a.n_bins0 ? b + 1 : b];
+    // per region: the prefix over the bin's tiles (in place)
+    for (uint32_t k = t; k < nsub; k += kGroupThreads) {
+        uint32_t run = 0;
+        for (uint32_t j = t0; j < t1; ++j) {
+            uint32_t* c = a.tcount + (size_t)j * nsub + k;
+            const uint32_t v = *c;
+            *c = run;
+            run += v;
+        }
+        tot[k] = run;
     }
     __syncthreads();
-    for (uint32_t lo = threadIdx.x; lo < nlo; lo += 256) {
-        const uint32_t b = (hi << a.d0) | lo;
-        if (b < a.n_bins) {
-            a.rstart[b] = s_lb[lo];
-            a.rend[b] = s_lb[lo + 1];
+    // the regions' starts: a contiguous chunk of regions per thread, one block scan
+    const uint32_t per = (nsub + kGroupThreads - 1) / kGroupThreads;
+    const uint32_t k0 = min(t * per, nsub), k1 = min(k0 + per, nsub);
+    uint32_t sum = 0;
+    for (uint32_t k = k0; k < k1; ++k) sum += tot[k];
+    uint32_t run = a.bin_base[b] + block_exclusive_scan<kGroupThreads>(sum, tmp, nullptr);
+    const uint32_t g0 = b << a.sub_bits;
+    for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t c = tot[k];
+        tot[k] = run;
+        if (g0 + k < a.n_regions) {
+            a.rstart[g0 + k] = run;
+            a.rend[g0 + k] = run + c;
+        }
+        run += c;
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < nsub; k += kGroupThreads) {
+        const uint32_t st = tot[k];
+        for (uint32_t j = t0; j < t1; ++j) a.tcount[(size_t)j * nsub + k] += st;
+    }
+}
+
+template <class Codec>
+__global__ __launch_bounds__(kGroupThreads) void k_gplace(GroupArgs a) {
+    using Rec = typename Codec::Rec;
+    extern __shared__ uint32_t gl[];                 // [waves][2^s0]: the tile's cursors
+    __shared__ GroupSub<Codec> G;
+    G.load(a);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t nsub = 1u << a.sub_bits, smask = nsub - 1u;
+    uint32_t* cw = gl + wid * nsub;
+    const Rec* __restrict__ in = (const Rec*)a.rec_in;
+    Rec* __restrict__ out = (Rec*)a.rec_out;
+    const uint32_t n_t = a.tile_base[a.n_bins0];
+    // Every lane loads and stores in every round (past the tile's end: the last record again,
+    // stored to the padding past the batch), and the next rounds' records are loaded before
+    // this round's stores: with no memory operation under a branch the wait-count pass counts
+    // statically, so waiting for a round's records does not drain the stores issued before it
+    // (one vmcnt for both on gfx950).
+    const uint32_t pad = a.pad + lane;
+    for (uint32_t t = blockIdx.x * kGroupWaves + wid; t < n_t; t += gridDim.x * kGroupWaves) {
+        uint32_t b, beg, end;
+        group_tile(a, t, b, beg, end);
+        const uint32_t* src = a.tcount + (size_t)t * nsub;
+        for (uint32_t k = lane; k < nsub; k += 64) cw[k] = src[k];
+        wave_fence();
+        auto load = [&](Rec (&r)[kGroupDepth], uint32_t i0) {
+#pragma unroll
+            for (int k = 0; k < kGroupDepth; ++k) {
+                const uint32_t i = i0 + (uint32_t)k * 64 + lane;
+                r[k] = ld_rec<kNtRgRec>(in + (i < end ? i : end - 1));
+            }
+        };
+        auto place = [&](const Rec (&r)[kGroupDepth], uint32_t i0) {
+#pragma unroll
+            for (int k = 0; k < kGroupDepth; ++k) {
+                const uint32_t i = i0 + (uint32_t)k * 64 + lane;
+                const bool act = i < end;
+                const uint32_t sb = act ? G.of(a, r[k], smask) : 0u;
+                const uint64_t m = wave_match(sb, (int)a.sub_bits, act);
+                const uint32_t lr = popc_below(m);
+                const uint32_t pos = cw[sb] + lr;
+                wave_fence();                            // every lane has read its cursor
+                if (act && lr == 0) cw[sb] = pos + (uint32_t)__popcll(m);
+                wave_fence();
+                const uint32_t wp = (a.ablate & kAblGroupSeq) ? i : pos;
+                st_rec<false>(out + (act ? wp : pad), r[k]);    // (temporal: sectors merge in L2)
+                st<kNtScPos>(a.pos_out + (act ? i : pad), act ? pos : 0u);
+            }
+        };
+        Rec ra[kGroupDepth], rb[kGroupDepth];
+        load(ra, beg);
+        for (uint32_t i0 = beg; i0 < end; i0 += 128 * kGroupDepth) {
+            load(rb, i0 + 64 * kGroupDepth);
+            place(ra, i0);
+            if (i0 + 64 * kGroupDepth >= end) break;     // (wave-uniform)
+            load(ra, i0 + 128 * kGroupDepth);
+            place(rb, i0 + 64 * kGroupDepth);
+        }
+        wave_fence();
+    }
+}
+
+// k_gplace with the tile's records sorted by region in LDS first, in chunks of kGChunk: the
+// global stores then go out as runs of consecutive records per region (a wave-instruction
+// covers a few lines instead of 64 scattered 16-B pieces: with every record scattered,
+// k_gplace ran 1.5 ms on sw_zipf, with the same stores made contiguous 0.9 ms). Each wave
+// ranks its own 256 records of the chunk (4 rounds, ballot match, wave-private counts), the
+// counts are scanned region-major then wave (stable), records go to their sorted slot in
+// LDS, and the chunk is written out in sorted order; the tile's cursors advance per chunk.
+// For bins of up to 2^kGLdsMaxSub regions (wider ones take k_gplace).
+constexpr int kGPThreads = 512;
+constexpr int kGPWaves = kGPThreads / 64;
+constexpr uint32_t kGChunk = 2048;                   // records sorted in LDS at once
+constexpr uint32_t kGLdsMaxSub = 10;
+template <class Rec>
+__host__ __device__ inline size_t gplace_lds_bytes(uint32_t sub_bits) {
+    const size_t nsub = (size_t)1 << sub_bits;
+    return kGChunk * sizeof(Rec) + kGChunk * 2 + kGPWaves * nsub * 2 + 2 * nsub * 4;
+}
+template <class Codec>
+__global__ __launch_bounds__(kGPThreads) void k_gplace_lds(GroupArgs a) {
+    using Rec = typename Codec::Rec;
+    extern __shared__ uint4 glds[];
+    __shared__ GroupSub<Codec> G;
+    __shared__ uint32_t s_tmp[kGPWaves];
+    const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const uint32_t nsub = 1u << a.sub_bits, smask = nsub - 1u;
+    Rec* stg = (Rec*)glds;                            // [kGChunk] the chunk, sorted
+    uint16_t* ssub = (uint16_t*)(stg + kGChunk);      // [kGChunk] their regions
+    uint16_t* hist = ssub + kGChunk;                  // [waves][nsub] counts, then wave prefixes
+    uint32_t* tsub = (uint32_t*)(hist + kGPWaves * nsub);   // [nsub] chunk-local region starts
+    uint32_t* gcur = tsub + nsub;                     // [nsub] the tile's global cursors
+    G.load(a);
+    const Rec* __restrict__ in = (const Rec*)a.rec_in;
+    Rec* __restrict__ out = (Rec*)a.rec_out;
+    const uint32_t n_t = a.tile_base[a.n_bins0];
+    const uint32_t per = (nsub + kGPThreads - 1) / kGPThreads;
+    const uint32_t k0 = min(t * per, nsub), k1 = min(k0 + per, nsub);
+    for (uint32_t tt = blockIdx.x; tt < n_t; tt += gridDim.x) {
+        uint32_t b, beg, end;
+        group_tile(a, tt, b, beg, end);
+        __syncthreads();                              // the previous tile's readers are done
+        for (uint32_t k = t; k < nsub; k += kGPThreads) gcur[k] = a.tcount[(size_t)tt * nsub + k];
+        for (uint32_t c0 = beg; c0 < end; c0 += kGChunk) {
+            const uint32_t c1 = min(c0 + kGChunk, end);
+            for (uint32_t k = t; k < kGPWaves * nsub; k += kGPThreads) hist[k] = 0;
+            // this wave's 256 records of the chunk: 4 rounds, loaded together
+            const uint32_t w0 = c0 + wid * 256u;
+            Rec r[4];
+            uint32_t sb[4], wr[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t j = w0 + (uint32_t)q * 64 + lane;
+                r[q] = ld_rec<kNtRgRec>(in + (j < c1 ? j : c1 - 1));
+            }
+            __syncthreads();                          // hist zeroed (and gcur loaded)
+            uint16_t* hw = hist + wid * nsub;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t j = w0 + (uint32_t)q * 64 + lane;
+                const bool act = j < c1;
+                sb[q] = act ? G.of(a, r[q], smask) : 0u;
+                const uint64_t m = wave_match(sb[q], (int)a.sub_bits, act);
+                const uint32_t lr = popc_below(m);
+                wr[q] = (uint32_t)hw[sb[q]] + lr;    // rank among this wave's records of the region
+                wave_fence();
+                if (act && lr == 0) hw[sb[q]] = (uint16_t)(wr[q] + (uint32_t)__popcll(m));
+                wave_fence();
+            }
+            __syncthreads();
+            // region-major, then wave: each region's start in the chunk, each wave's offset in it
+            uint32_t sum = 0;
+            for (uint32_t k = k0; k < k1; ++k) {
+                uint32_t run = 0;
+                for (uint32_t w = 0; w < (uint32_t)kGPWaves; ++w) {
+                    const uint32_t v = hist[w * nsub + k];
+                    hist[w * nsub + k] = (uint16_t)run;
+                    run += v;
+                }
+                tsub[k] = run;                        // (the region's count, for now)
+                sum += run;
+            }
+            uint32_t base = block_exclusive_scan<kGPThreads>(sum, s_tmp, nullptr);
+            for (uint32_t k = k0; k < k1; ++k) {
+                const uint32_t c = tsub[k];
+                tsub[k] = base;
+                base += c;
+            }
+            __syncthreads();
+            // sorted slots in LDS; the final position of every pass-0 position
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t j = w0 + (uint32_t)q * 64 + lane;
+                if (j < c1) {
+                    const uint32_t o = (uint32_t)hist[wid * nsub + sb[q]] + wr[q];
+                    stg[tsub[sb[q]] + o] = r[q];
+                    ssub[tsub[sb[q]] + o] = (uint16_t)sb[q];
+                    st<kNtScPos>(a.pos_out + j, gcur[sb[q]] + o);
+                }
+            }
+            __syncthreads();
+            // the chunk in sorted order: runs of consecutive records per region
+            for (uint32_t i = t; i < c1 - c0; i += kGPThreads) {
+                const uint32_t k = ssub[i];
+                st_rec<false>(out + gcur[k] + (i - tsub[k]), stg[i]);
+            }
+            __syncthreads();
+            // the tile's cursors past this chunk
+            for (uint32_t k = k0; k < k1; ++k) {
+                const uint32_t nx = k + 1 < nsub ? tsub[k + 1] : c1 - c0;
+                gcur[k] += nx - tsub[k];
+            }
         }
     }
 }
@@ -528,13 +801,16 @@ __global__ __launch_bounds__(256) void k_bin_bounds(BoundsArgs a) {
 // ------------------------------------------------------------------ routing helpers
 // After the pass-0 scan: the routed bins' ranges (pass 1 reuses bin_base / bin_total) and
 // the number of normal records, which pass 1 and the unpermute read on device.
-__global__ __launch_bounds__(1024) void k_route_ranges(const uint32_t* __restrict__ bin_base,
+__global__ __launch_bounds__(1024) void k_route_ranges(const uint32_t* __restrict__ route_list,
+                                                       const uint32_t* __restrict__ bin_base,
                                                        const uint32_t* __restrict__ bin_total,
                                                        uint32_t lo_bins, uint32_t* route_start,
                                                        uint32_t* route_cnt, BatchCtl* ctl) {
     for (uint32_t i = threadIdx.x; i < kRouteSlots; i += blockDim.x) {
-        route_start[i] = bin_base[lo_bins + i];
-        route_cnt[i] = bin_total[lo_bins + i];
+        const bool used = route_list[i] != kNone;
+        const uint32_t bn = lo_bins + (used ? route_list[kRouteSlots + i] : 0u);
+        route_start[i] = used ? bin_base[bn] : 0u;
+        route_cnt[i] = used ? bin_total[bn] : 0u;
     }
     if (threadIdx.x == 0) ctl->n_normal = bin_base[lo_bins];
 }
@@ -783,8 +1059,7 @@ hipError_t launch_upsweep(const PartArgs& a, bool raw, bool wide, hipStream_t s)
         if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, true, false>), grid, block, lds, s, a);
         else hipLaunchKernelGGL((k_upsweep<CodecC, true, false>), grid, block, lds, s, a);
     } else {
-        if (wide) hipLaunchKernelGGL((k_upsweep<CodecW, false, false>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((k_upsweep<CodecC, false, false>), grid, block, lds, s, a);
+        return hipErrorInvalidValue;         // (record-input passes: k_group since round 6)
     }
     return hipGetLastError();
 }
@@ -797,23 +1072,15 @@ hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s)
         const dim3 b2(2 * kTileThreads);
         const size_t lc = split_stage_off<CodecC>(bins) * 8 + 2 * kTileThreads * (sizeof(RecC) + 2);
         const size_t lw = split_stage_off<CodecW>(bins) * 8 + 2 * kTileThreads * (sizeof(RecW) + 2);
-        if (raw) {
-            if (wide) hipLaunchKernelGGL((k_scatter_split<CodecW, true>), grid, b2, lw, s, a);
-            else hipLaunchKernelGGL((k_scatter_split<CodecC, true>), grid, b2, lc, s, a);
-        } else {
-            if (wide) hipLaunchKernelGGL((k_scatter_split<CodecW, false>), grid, b2, lw, s, a);
-            else hipLaunchKernelGGL((k_scatter_split<CodecC, false>), grid, b2, lc, s, a);
-        }
+        if (!raw) return hipErrorInvalidValue;   // (record-input passes: k_group since round 6)
+        if (wide) hipLaunchKernelGGL((k_scatter_split<CodecW, true>), grid, b2, lw, s, a);
+        else hipLaunchKernelGGL((k_scatter_split<CodecC, true>), grid, b2, lc, s, a);
         return hipGetLastError();
     }
     const size_t lds = bins * (sizeof(uint64_t) + sizeof(uint32_t));
-    if (raw) {
-        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, lds, s, a);
-    } else {
-        if (wide) hipLaunchKernelGGL((k_scatter<CodecW, false>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((k_scatter<CodecC, false>), grid, block, lds, s, a);
-    }
+    if (!raw) return hipErrorInvalidValue;
+    if (wide) hipLaunchKernelGGL((k_scatter<CodecW, true>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((k_scatter<CodecC, true>), grid, block, lds, s, a);
     return hipGetLastError();
 }
 
@@ -866,12 +1133,25 @@ hipError_t launch_stats_reduce(unsigned long long* stats, BatchCtl* ctl, hipStre
     return hipGetLastError();
 }
 
-hipError_t launch_bin_bounds(const BoundsArgs& a, bool wide, hipStream_t s) {
-    if (a.n_bins == 0 || a.d0 > kMaxDigitBits || a.d1 > kMaxDigitBits || a.d0 < 1)
+hipError_t launch_group(const GroupArgs& a, bool wide, hipStream_t s) {
+    if (a.n_bins0 == 0 || a.sub_bits > (uint32_t)kMaxDigitBits || a.max_tiles == 0)
         return hipErrorInvalidValue;
-    const dim3 g(1u << a.d1), b(256);
-    if (wide) hipLaunchKernelGGL(k_bin_bounds<CodecW>, g, b, 0, s, a);
-    else hipLaunchKernelGGL(k_bin_bounds<CodecC>, g, b, 0, s, a);
+    const size_t nsub = (size_t)1 << a.sub_bits;
+    const size_t lds = kGroupWaves * nsub * sizeof(uint32_t);
+    // one wave per tile: a persistent grid over the (device-counted) tiles
+    const dim3 gw(persistent_grid((a.max_tiles + kGroupWaves - 1) / kGroupWaves, 8)), b(kGroupThreads);
+    hipLaunchKernelGGL(k_gtiles, dim3(1), dim3(1024), 0, s, a);
+    if (wide) hipLaunchKernelGGL(k_gcount<CodecW>, gw, b, lds, s, a);
+    else hipLaunchKernelGGL(k_gcount<CodecC>, gw, b, lds, s, a);
+    hipLaunchKernelGGL(k_gscan, dim3(a.n_bins0), b, nsub * sizeof(uint32_t), s, a);
+    if (a.sub_bits <= kGLdsMaxSub && !(a.ablate & kAblGroupSeq)) {
+        const dim3 gp(persistent_grid((a.max_tiles + 1) / 2, 4)), bp(kGPThreads);
+        if (wide) hipLaunchKernelGGL(k_gplace_lds<CodecW>, gp, bp, gplace_lds_bytes<RecW>(a.sub_bits), s, a);
+        else hipLaunchKernelGGL(k_gplace_lds<CodecC>, gp, bp, gplace_lds_bytes<RecC>(a.sub_bits), s, a);
+        return hipGetLastError();
+    }
+    if (wide) hipLaunchKernelGGL(k_gplace<CodecW>, gw, b, lds, s, a);
+    else hipLaunchKernelGGL(k_gplace<CodecC>, gw, b, lds, s, a);
     return hipGetLastError();
 }
 
@@ -881,10 +1161,11 @@ static void unpermute_mid(const UnpermArgs& a, hipStream_t s) {
                        (const Res*)a.res, (Res*)a.mid, a.n, a.ctl, a.mid_xcd);
 }
 
-hipError_t launch_route_ranges(const uint32_t* bin_base, const uint32_t* bin_total, uint32_t lo_bins,
-                               uint32_t* route_start, uint32_t* route_cnt, BatchCtl* ctl, hipStream_t s) {
-    hipLaunchKernelGGL(k_route_ranges, dim3(1), dim3(1024), 0, s, bin_base, bin_total, lo_bins,
-                       route_start, route_cnt, ctl);
+hipError_t launch_route_ranges(const uint32_t* route_list, const uint32_t* bin_base,
+                               const uint32_t* bin_total, uint32_t lo_bins, uint32_t* route_start,
+                               uint32_t* route_cnt, BatchCtl* ctl, hipStream_t s) {
+    hipLaunchKernelGGL(k_route_ranges, dim3(1), dim3(1024), 0, s, route_list, bin_base, bin_total,
+                       lo_bins, route_start, route_cnt, ctl);
     return hipGetLastError();
 }
 

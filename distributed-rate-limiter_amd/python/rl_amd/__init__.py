@@ -398,6 +398,14 @@ class Engine:
             raise RlError(k, "rl_debug_fetch")
         return out[:k]
 
+    def debug_bin_totals(self):
+        """The last batch's pass-0 bin sizes (2^kMaxDigitBits entries; the unused ones stale)."""
+        out = np.zeros(1 << 13, np.uint32)
+        k = self._L.rl_debug_fetch(self._h, b"bin_totals", _p(out), out.nbytes)
+        if k < 0:
+            raise RlError(k, "rl_debug_fetch")
+        return out[:k]
+
     def sync(self):
         st = self._L.rl_sync(self._h)
         if st != RL_OK:

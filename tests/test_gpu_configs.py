@@ -209,6 +209,17 @@ def test_config_tb_uniform_pipelined():
     assert 0 < got[0].sum() < len(k)
 
 
+@pytest.mark.timeout(400)
+def test_config_sw_zipf_pipelined_routed():
+    """configs[2]'s workload in 8 back-to-back pipelined batches of 2^24: with RL_OPT_PIPELINE
+    batch k routes the hot regions of batch k - 2 (the route table of its scratch set, round 6),
+    so from batch 2 on pass 0 sends them straight to their final bins while batch k - 1's region
+    stage still runs."""
+    k, got, st = run_config("sw_zipf", 1 << 27, 8, pipeline=True)
+    assert st["routed"] > 0 and st["hot_regions"] > 0, st
+    assert 0 < got[0].sum() < len(k)
+
+
 def test_config_mixed_tenants_pipelined_ragged():
     """Pipelined batches of ragged, growing sizes: each scratch set is regrown mid-stream
     (two passes, hot path, 10 limiters), and a tiny batch sits between large ones."""

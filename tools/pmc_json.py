@@ -44,6 +44,8 @@ def stage_of(name: str):
         return "region"
     if "k_unpermute<" in name or "k_unpermute_split<" in name:
         return "unpermute"
+    if "k_group<" in name:
+        return "group"
     if "k_unpermute_mid<" in name:
         return "unpermute_mid"
     if "k_hot_chains<" in name:
