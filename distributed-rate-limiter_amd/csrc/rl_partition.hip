@@ -321,7 +321,11 @@ template <class Codec>
 __host__ __device__ inline size_t split_stage_off(uint32_t bins) {     // in u64 words, 16-B aligned
     return ((size_t)bins + (bins + 1) / 2 + 1) & ~(size_t)1;
 }
-template <class Codec, bool RAW>
+// ABL (measurement-only instantiations, rl_tune ablate bits 20-25; results wrong): 1 no record
+// store, 2 no position store, 4 records stored at their input index, 8 no ballot match,
+// 16 no encode (the key as the record, digit 0 + lane), 32 whole sectors (each lane its
+// record to both halves of its 32-B sector)
+template <class Codec, bool RAW, int ABL = 0>
 __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) {
     using Rec = typename Codec::Rec;
     constexpr int kRecV = (int)(sizeof(Rec) / 16);
@@ -353,6 +357,11 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
         rec = Rec{};
         d = 0;
         if (i >= n) return;
+        if constexpr (RAW && (ABL & 16)) {
+            rec.h = in.key;
+            d = (i & 63u) % (a.n_bins_pass ? a.n_bins_pass : 1u);
+            return;
+        }
         if constexpr (RAW) {
             uint32_t lim = in.lim_v(a), op = in.op_v(a);
             const int32_t p = in.permits;
@@ -434,7 +443,7 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
 #pragma unroll
                 for (int k = 0; k < kRecV; ++k) rv[k] = ((const u32x4_t*)stg)[sl * kRecV + k];
                 const uint32_t d = sdg[sl];
-                const uint64_t m = wave_match(d, a.digit_bits, active);
+                const uint64_t m = (ABL & 8) ? (active ? 1ULL << lane : 0ULL) : wave_match(d, a.digit_bits, active);
                 const uint32_t lr = popc_below(m);
                 const uint32_t cnt = (uint32_t)__popcll(m);
                 const bool leader = active && lr == 0;
@@ -451,11 +460,19 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
                     atomicAdd(&cur[d], cnt);
                     ((uint8_t*)&cntw[d])[wid] = 0;
                 }
-                const uint32_t wpos = active ? pos : a.n + lt;
-                Rec* dst = out_norm + ((active && d >= lo_route ? route_off : 0) + wpos);
+                const uint32_t wpos = (ABL & 4) ? (active ? i : a.n + lt) : active ? min(pos, last) : a.n + lt;
+                Rec* dst = out_norm + ((active && d >= lo_route && !(ABL & 4) ? route_off : 0) + wpos);
+                if constexpr ((ABL & 32) && kRecV == 1) {
+                    // whole 32-B sectors: the lane writes its record to both halves of its
+                    // sector (twice the store lanes, no partial sector)
+                    u32x4_t* sec = (u32x4_t*)(out_norm + ((active && d >= lo_route ? route_off : 0) + (wpos & ~1u)));
+                    sec[0] = rv[0];
+                    sec[1] = rv[0];
+                } else if constexpr (!(ABL & 1)) {
 #pragma unroll
-                for (int k = 0; k < kRecV; ++k) ((u32x4_t*)dst)[k] = rv[k];
-                st<kNtScPos>(a.pos_out + (active ? i : a.n + lt), pos);
+                    for (int k = 0; k < kRecV; ++k) ((u32x4_t*)dst)[k] = rv[k];
+                }
+                if constexpr (!(ABL & 2)) st<kNtScPos>(a.pos_out + (active ? i : a.n + lt), pos);
             }
         }
     }
@@ -1068,6 +1085,22 @@ hipError_t launch_scatter(const PartArgs& a, bool raw, bool wide, hipStream_t s)
     dim3 grid(persistent_grid(a.n_tiles, a.sc_per_cu ? a.sc_per_cu : 1)), block(kTileThreads);
     const uint32_t bins = a.n_bins_pass ? a.n_bins_pass : 1u << a.digit_bits;
     if (bins > (1u << kMaxDigitBits)) return hipErrorInvalidValue;
+    if (a.sc_split && (a.ablate >> 20) && raw && !wide) {   // measurement-only variants
+        const dim3 b2(2 * kTileThreads);
+        const size_t lc = split_stage_off<CodecC>(bins) * 8 + 2 * kTileThreads * (sizeof(RecC) + 2);
+        switch ((a.ablate >> 20) & 63u) {
+            case 1: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 1>), grid, b2, lc, s, a); break;
+            case 2: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 2>), grid, b2, lc, s, a); break;
+            case 3: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 3>), grid, b2, lc, s, a); break;
+            case 4: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 4>), grid, b2, lc, s, a); break;
+            case 8: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 8>), grid, b2, lc, s, a); break;
+            case 16: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 16>), grid, b2, lc, s, a); break;
+            case 27: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 27>), grid, b2, lc, s, a); break;
+            case 32: hipLaunchKernelGGL((k_scatter_split<CodecC, true, 32>), grid, b2, lc, s, a); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (a.sc_split && !a.ablate) {
         const dim3 b2(2 * kTileThreads);
         const size_t lc = split_stage_off<CodecC>(bins) * 8 + 2 * kTileThreads * (sizeof(RecC) + 2);
