@@ -205,7 +205,9 @@ def load_pmc(config_name, kernel, batch, world):
         d = s.get(config_name, {})
         if d.get("batch") != batch or d.get("world", 1) != world:
             return None, None
-        k = d.get(kernel)
+        # the step's traffic in the steady state (batches 1..: the timed steps all route hot
+        # regions; batch 0 does not), else over every profiled batch
+        k = d.get(kernel + "_steady", d.get(kernel)) if kernel == "step" else d.get(kernel)
         return (None, None) if k is None else (float(k["hbm_bytes_per_launch"]),
                                                s.get("_meta", {}).get(config_name))
     except Exception:

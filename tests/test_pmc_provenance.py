@@ -29,6 +29,9 @@ def test_summary_recomputes_from_named_dir(config):
     st = pmc_json.summarize(d)
     for k in ("fetch_bytes", "write_bytes", "hbm_bytes_per_launch", "steps"):
         assert math.isclose(st["step"][k], ent["step"][k], rel_tol=1e-12), (config, k)
+    if "step_steady" in ent:
+        for k in ("fetch_bytes", "write_bytes", "hbm_bytes_per_launch"):
+            assert math.isclose(st["step_steady"][k], ent["step_steady"][k], rel_tol=1e-12), (config, k)
     for stage, v in st.items():
         if isinstance(v, dict) and "avg_us" in v and stage in ent:
             assert math.isclose(v["avg_us"], ent[stage]["avg_us"], rel_tol=1e-12), (config, stage)

@@ -121,6 +121,26 @@ def summarize(base):
         st["step"] = {"fetch_bytes": tot["FETCH_SIZE"] * 1024 * 2 / steps,
                       "write_bytes": tot["WRITE_SIZE"] * 1024 / steps, "steps": steps}
         st["step"]["hbm_bytes_per_launch"] = st["step"]["fetch_bytes"] + st["step"]["write_bytes"]
+    # The steady state: batches 1.. only (batch 0 is the bench's first warmup step: no routed
+    # regions yet, so every record takes the grouping pass; the timed steps all route). A
+    # batch starts at its pass-0 upsweep (dispatch order).
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    for f, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        p = _csv(base, f, f"{f}_counter_collection.csv")
+        if p is None:
+            continue
+        b = -1
+        for r in sorted(csv.DictReader(open(p)), key=lambda r: int(r["Dispatch_Id"])):
+            if stage_of(r["Kernel_Name"]) == "upsweep0":
+                b += 1
+            if b >= 0 and "k_synth" not in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                per[b][ctr] += float(r["Counter_Value"])
+    bs = [b for b in sorted(per) if b >= 1 and "FETCH_SIZE" in per[b] and "WRITE_SIZE" in per[b]]
+    if bs:
+        fb = sum(per[b]["FETCH_SIZE"] for b in bs) * 1024 * 2 / len(bs)
+        wb = sum(per[b]["WRITE_SIZE"] for b in bs) * 1024 / len(bs)
+        st["step_steady"] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
+                             "batches": bs}
     return st
 
 
