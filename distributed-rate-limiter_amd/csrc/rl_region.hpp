@@ -41,6 +41,9 @@ struct RegionLds : RegionTable {
 template <class Codec>
 struct RegionLds<Codec, false> : RegionTable {};
 
+// Image regions keep dead slots as tombstones until live + dead slots exceed this many (of
+// 256), then drop them and relink (the sparse path rebuilds on long probe chains instead).
+constexpr uint32_t kTombCrowd = 192;
 constexpr bool kSparseOn = true;                 // (rl_tune ablate kAblNoProbe turns it off at run time)
 
 // Sparse region (few records): the LDS table starts with every bucket kOccUnloaded and a
@@ -583,6 +586,7 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     // distinct key) instead of moving the 8 KB image both ways.
     const bool sparse = kSparseOn && cnt <= a.sparse_max && !(a.ablate & kAblNoProbe);
     SparseSrc sp{sparse ? tab : nullptr, xtab, batch_min, false};
+    bool tombs = false;                              // an image region kept dead slots as tombstones
     // rebuild the LDS table from registers: linear probing from each key's home
     auto rebuild = [&](const Slot (&img)[NS / 64], const uint64_t (&xim)[NS / 64], const bool (&keep)[NS / 64]) {
 #pragma unroll
@@ -605,9 +609,14 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
         for (uint32_t i = 0; i < NS / 64; ++i) { S.occ[lane + 64 * i] = kOccUnloaded; S.pm[lane + 64 * i] = 0; }
         wave_fence();
     } else {
-        // load the region in place, dropping entries no request of this batch can see: live
-        // keys keep their slots, so only the slots this batch changes are written back
-        bool cut = false;
+        // load the region in place: live keys keep their slots, so only the slots this batch
+        // changes are written back. Entries no request of this batch can see stay where they
+        // are as tombstones (claimable by an insert, never a hit; in HBM a dead slot that is
+        // not zero already is one): dropping them would need the relink below, which moved
+        // most keys of a region whose window rolled over (sw_zipf's steady state: region load
+        // 3.6 -> 13 us). Only once live + dead slots crowd the region (> kTombCrowd) are the
+        // dead ones dropped and the chains relinked.
+        uint32_t n_live = 0, n_dead = 0;
 #pragma unroll
         for (uint32_t i = 0; i < NS / 64; ++i) {
             const uint32_t s = lane + 64 * i;
@@ -615,14 +624,29 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
             const uint64_t x = xtab ? xtab[s] : 0;
             const bool fr = slot_free(v, x);
             const bool kp = !fr && slot_live(L, v, batch_min, x);
-            S.occ[s] = kp ? kOccUsed : fr ? 0u : kOccDirty;
+            S.occ[s] = kp ? kOccUsed : fr ? 0u : (kOccUsed | kOccTomb);
             S.pm[s] = 0;
             S.tag[s] = v.tag; S.sa[s] = v.a; S.sb[s] = v.b; S.sc[s] = v.c;
             if constexpr (LdsT::kCache) S.sx[s] = x;
-            cut |= !fr && !kp;
+            n_live += kp ? 1u : 0u;
+            n_dead += !fr && !kp ? 1u : 0u;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            n_live += __shfl_xor(n_live, o, 64);
+            n_dead += __shfl_xor(n_dead, o, 64);
+        }
+        if (n_dead != 0 && n_live + n_dead > kTombCrowd) {
+#pragma unroll
+            for (uint32_t i = 0; i < NS / 64; ++i) {
+                const uint32_t s = lane + 64 * i;
+                if (S.occ[s] & kOccTomb) S.occ[s] = kOccDirty;
+            }
+            wave_fence();
+            relink(S, lane);
+            n_dead = 0;
         }
         wave_fence();
-        if (__any(cut)) relink(S, lane);
+        tombs = n_dead != 0;
     }
 
     uint32_t n_allowed = 0, n_invalid = 0, n_caperr = 0, n_rounds = 0, n_hits = 0;
@@ -658,11 +682,12 @@ __device__ inline void region_body_t(const RegionArgs& a, uint32_t g, LdsT& S) {
     };
     using SpOn = std::integral_constant<bool, kSparseOn>;
     using SpOff = std::integral_constant<bool, false>;
+    // (tombstones need the sparse probe's checks; an image region holds no unloaded bucket)
     if (L.algo == kAlgoTB) {
-        if (sparse) stream(std::integral_constant<int, kAlgoTB>{}, SpOn{});
+        if (sparse || tombs) stream(std::integral_constant<int, kAlgoTB>{}, SpOn{});
         else stream(std::integral_constant<int, kAlgoTB>{}, SpOff{});
     } else {
-        if (sparse) stream(std::integral_constant<int, kAlgoSW>{}, SpOn{});
+        if (sparse || tombs) stream(std::integral_constant<int, kAlgoSW>{}, SpOn{});
         else stream(std::integral_constant<int, kAlgoSW>{}, SpOff{});
     }
     wave_fence();
