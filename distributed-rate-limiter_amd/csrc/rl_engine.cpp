@@ -123,6 +123,7 @@ struct rl_engine {
     bool route = true;                      // rl_tune("route")
     bool region_order = true;               // rl_tune("region_order"): largest regions dispatched first
     uint32_t order_prefix = 4096;           // rl_tune("order_prefix"): ... after this many of the smallest
+    uint32_t tile_items = 0;                // rl_tune("tile_items"): partition tile rounds (0: auto)
     uint32_t group_bits = 12;               // rl_tune("group_bits"): two-pass batches' pass-0
                                             // high digit (2^12 bins + the routed ones)
     uint32_t* order = nullptr;              // [order_cap + 1]
@@ -621,7 +622,15 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         max_any = std::max<int64_t>(max_any, l.cfg.max_permits);
     }
     const int res_bytes = res_bytes_for(max_any, wide);
-    const uint32_t nt = (uint32_t)((n + kTile - 1) / kTile);
+    // partition tiles of 128K requests for large batches (half the [bin][tile] counts to write
+    // and scan: sw_zipf's 2^28-request batches, scan0 0.16 -> 0.06 ms, upsweep0 0.89 -> 0.75 ms),
+    // 64K below (tb_uniform's 2^26 needs the 1024 tiles to keep every CU busy; the unpermute keeps
+    // 64K tiles: run_r06o.sh)
+    const uint32_t titems = e->tile_items ? e->tile_items
+                                          : (n >= ((size_t)3 << 26) ? 2u * kTileItems : (uint32_t)kTileItems);
+    const size_t tile_n = (size_t)titems * kTileThreads;
+    const uint32_t nt = (uint32_t)((n + tile_n - 1) / tile_n);
+    const uint32_t nt_un = (uint32_t)((n + kTile - 1) / kTile);
     bool cache = false;
     for (auto& l : e->lims) cache |= l.dev.cache_ttl_ms > 0;
     const uint32_t n_bins = e->n_regions;            // one partition bin per region
@@ -698,7 +707,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     mark_on(e, ps, 0);
     PartArgs pa{};
     pa.key = key; pa.permits = permits; pa.now_ns = now_ns; pa.limiter = limiter; pa.op = op;
-    pa.n = (uint32_t)n; pa.n_tiles = nt; pa.n_lim = (uint32_t)e->lims.size();
+    pa.n = (uint32_t)n; pa.n_tiles = nt; pa.tile_items = titems; pa.n_lim = (uint32_t)e->lims.size();
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = B.d_ctl;
     pa.counts = B.counts; pa.bin_base = B.bin_base; pa.ablate = e->ablate;
     pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu; pa.sc_split = e->sc_split;
@@ -844,7 +853,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     ua.tok = tokens_after ? B.tok : nullptr;
     ua.ext = B.ext; ua.ctl = B.d_ctl;
     ua.allowed = allowed; ua.remaining = remaining; ua.tokens_out = tokens_after;
-    ua.n = (uint32_t)n; ua.n_tiles = nt; ua.ablate = e->ablate; ua.per_cu = e->un_per_cu;
+    ua.n = (uint32_t)n; ua.n_tiles = nt_un; ua.ablate = e->ablate; ua.per_cu = e->un_per_cu;
     ua.split = e->un_split == 1 || (e->un_split == 2 && passes == 2);
     ua.mid_xcd = e->mid_xcd;
     HIP_OK(launch_unpermute(ua, res_bytes, s));
@@ -1178,6 +1187,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "route") == 0) {             // hot-region routing in pass 0
         e->route = value != 0;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "tile_items") == 0) {        // partition tile = value x 512 requests
+        if (value != 0 && (value < 8 || value > 1024 || value % 8 != 0)) return RL_E_INVALID_ARG;
+        e->tile_items = (uint32_t)value;
         return RL_OK;
     }
     if (std::strcmp(key, "group_bits") == 0) {        // two-pass batches: pass-0 high-digit bits

@@ -69,6 +69,8 @@ struct PartArgs {
     uint32_t* pos_out;         // pos_out[i] = destination of element i
     uint32_t n;
     uint32_t n_tiles;
+    uint32_t tile_items;       // rounds of kTileThreads requests per tile (kTileItems, or twice
+                               // it for large batches: fewer [bin][tile] counts to write and scan)
     uint32_t n_lim;
     int32_t shard_bits;
     const DevLimiter* lims;

@@ -44,10 +44,11 @@ __global__ __launch_bounds__(kTileThreads) void k_upsweep(PartArgs a) {
         if (tile >= a.n_tiles) break;
         for (uint32_t b = t; b < bins; b += kTileThreads) hist[b] = 0;
         __syncthreads();
-        if (tile * (uint64_t)kTile < n) {
+        const uint32_t items = a.tile_items, T = items * (uint32_t)kTileThreads;
+        if (tile * (uint64_t)T < n) {
 #pragma unroll 8
-            for (int r = 0; r < kTileItems; ++r) {
-                const uint32_t i = tile * (uint32_t)kTile + (uint32_t)r * kTileThreads + t;
+            for (uint32_t r = 0; r < items; ++r) {
+                const uint32_t i = tile * T + r * (uint32_t)kTileThreads + t;
                 if (i < n) {
                     const uint32_t g = bin_of<Codec, RAW>(a, i, L);
                     const uint32_t d = pass_digit(a, g, R);
@@ -162,7 +163,7 @@ __device__ inline void scatter_outputs(const PartArgs& a, Rec*& out_norm, int64_
     lo_route = a.route_list ? a.lo_bins : 0xFFFFFFFFu;
 }
 
-constexpr int kScatterDepth = 8;   // rounds of inputs in flight (divides kTileItems)
+constexpr int kScatterDepth = 8;   // rounds of inputs in flight (divides tile_items)
 
 template <class Codec, bool RAW>
 __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
     for (uint32_t it = 0;; ++it) {
         const uint32_t tile = tile_at(it, a.n_tiles);
         if (tile >= a.n_tiles) break;
-        const uint32_t tile0 = tile * (uint32_t)kTile;
+        const uint32_t tile0 = tile * a.tile_items * (uint32_t)kTileThreads;
         if (tile0 >= n) continue;                        // (workgroup-uniform)
         __syncthreads();     // previous tile's LDS users are done
         for (uint32_t b = t; b < bins; b += kTileThreads) {
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
         // move would wait on its load). vmcnt retires loads and stores in issue order, so
         // waiting for round r's inputs also waits for the scattered stores issued before
         // them: a deep ring spreads that store-ack latency over kScatterDepth rounds.
-        for (int r = 0; r < kTileItems; r += kScatterDepth) {
+        for (int r = 0; r < (int)a.tile_items; r += kScatterDepth) {
 #pragma unroll
             for (int k = 0; k < kScatterDepth; ++k) {
                 round(in[k], r + k);
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
 // encode each round and stage its records and digits in LDS one round ahead; the ranking
 // waves (threads 0..kTileThreads-1) read them from LDS, rank, and store — they issue no
 // global load inside a tile, so nothing ever waits behind their stores.
-constexpr int kSplitDepth = 4;       // loader rounds in flight (divides kTileItems)
+constexpr int kSplitDepth = 4;       // loader rounds in flight (divides tile_items)
 template <class Codec>
 __host__ __device__ inline size_t split_stage_off(uint32_t bins) {     // in u64 words, 16-B aligned
     return ((size_t)bins + (bins + 1) / 2 + 1) & ~(size_t)1;
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
     for (uint32_t it = 0;; ++it) {
         const uint32_t tile = tile_at(it, a.n_tiles);
         if (tile >= a.n_tiles) break;
-        const uint32_t tile0 = tile * (uint32_t)kTile;
+        const uint32_t tile0 = tile * a.tile_items * (uint32_t)kTileThreads;
         if (tile0 >= n) continue;                        // (workgroup-uniform)
         __syncthreads();     // previous tile's LDS users are done
         // The two roles run separate loops with the same barriers (1 + 2 per round), so the
@@ -428,14 +429,14 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
                 __syncthreads();
                 __syncthreads();
             };
-            for (int r = 0; r < kTileItems; r += kSplitDepth) {
+            for (int r = 0; r < (int)a.tile_items; r += kSplitDepth) {
 #pragma unroll
                 for (int k = 0; k < kSplitDepth; ++k) stage(r + k, in[(k + 1) % kSplitDepth]);
             }
         } else {
             for (uint32_t b = lt; b < bins; b += kTileThreads) cntw[b] = 0;
             __syncthreads();
-            for (int r = 0; r < kTileItems; ++r) {
+            for (int r = 0; r < (int)a.tile_items; ++r) {
                 const uint32_t i = tile0 + (uint32_t)r * kTileThreads + lt;
                 const bool active = i < n;
                 const uint32_t sl = (uint32_t)(r & 1) * kTileThreads + lt;
