@@ -112,6 +112,7 @@ struct rl_engine {
     uint32_t walk_hint = 0;                 // listed regions that wanted a walk in the last batch
                                             // seen complete (walk_tab is allocated once it is > 0)
     uint32_t walk_min = kWalkMinAllows;     // rl_tune("walk_min"): fewest expected allows walked
+    bool chain_split = false;               // rl_tune("chain_split"): two-wave hot chains
     uint32_t* hot_mark = nullptr;           // [hot_mark_cap] epoch marks per bin
     size_t hot_mark_cap = 0;
     uint32_t epoch = 0;
@@ -783,6 +784,7 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     // chain launch size: twice the hot count of the last batch the host saw complete (a
     // hint only: the chains loop over the hot list with the grid's stride), the whole
     // kHotMax before any batch has completed
+    ra.chain_split = e->chain_split ? 1u : 0u;
     if (e->hot_hint != 0xFFFFFFFFu) {
         const uint32_t nh = e->hot_hint;
         ra.chain_grid = nh ? std::min<uint32_t>(kHotMax, std::max<uint32_t>(256u, 2u * nh)) : 64u;
@@ -1206,6 +1208,10 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
             if (e->hstream) HIP_OK(hipStreamSynchronize(e->hstream));
             dfree(e->walk_tab);
         }
+        return RL_OK;
+    }
+    if (std::strcmp(key, "chain_split") == 0) {       // a hot region's other keys on a second wave
+        e->chain_split = value != 0;
         return RL_OK;
     }
     if (std::strcmp(key, "walk_min") == 0) {          // keys walked: at least this many allows expected

@@ -447,13 +447,18 @@ __global__ __launch_bounds__(256) void k_hot_summ(RegionArgs a) {
 // arrival order, 64 records at a time through wave_apply. (A workgroup of one wave per pass
 // waited for its wave slots on one CU beside the normal regions: sw_zipf's later chains
 // started ~4 ms into the stage.)
-template <class Codec, class Res, bool TOK>
+// SPLIT (two-wave workgroups): wave 0 loads the region and runs pass 1, wave 1 runs pass 2
+// beside it on the same LDS image (pass 1 touches only its keys' slots, pass 2 never those)
+// and exits, handing its debug words over in LDS; wave 0 waits for it and writes back.
+template <class Codec, class Res, bool TOK, bool SPLIT>
 __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Codec, true>& S) {
     using Rec = typename Codec::Rec;
     constexpr uint32_t NS = kRegionSlots;
     __shared__ int32_t s_hslot[2];
+    __shared__ uint64_t s_p2[3];                      // SPLIT: wave 1 done, its cycles, records
     const uint32_t hc = min(a.hot_count[0], kHotMax);
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = SPLIT ? threadIdx.x >> 6 : 0u;
     if (i >= hc) return;
     // the passes are sequential critical paths beside thousands of normal-region waves
     __builtin_amdgcn_s_setprio(3);
@@ -475,7 +480,7 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
     }
     const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
     RL_GLOBAL Slot* tab = as_global((Slot*)L.table + (size_t)(region - L.region_base) * NS);
-    {
+    if (wv == 0) {
         // ---- load + rebuild the region (as k_regions), find or insert the hot key's slot
         Slot img[NS / 64];
 #pragma unroll
@@ -514,8 +519,10 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
             hsl[k] = hslot;
         }
         if (lane == 0) { s_hslot[0] = hsl[0]; s_hslot[1] = hsl[1]; }
+        if (SPLIT && lane == 0) s_p2[0] = 0;
     }
-    wave_fence();
+    if (SPLIT) __syncthreads();
+    else wave_fence();
     // hot_ok false (no dominant key, or its region is full): pass 2 takes every record; the
     // second key has a chain only beside the first's
     const int32_t hsl0 = s_hslot[0];
@@ -1519,13 +1526,13 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         if (a.dbg) cyc_pass2 += __builtin_amdgcn_s_memtime() - c_p2;
     };
     if (L.algo == kAlgoTB) {
-        if (hot_ok) pass1(std::integral_constant<int, kAlgoTB>{}, 0u);
-        if (hot_ok2) pass1(std::integral_constant<int, kAlgoTB>{}, 1u);
-        pass2(std::integral_constant<int, kAlgoTB>{});
+        if (wv == 0 && hot_ok) pass1(std::integral_constant<int, kAlgoTB>{}, 0u);
+        if (wv == 0 && hot_ok2) pass1(std::integral_constant<int, kAlgoTB>{}, 1u);
+        if (!SPLIT || wv == 1) pass2(std::integral_constant<int, kAlgoTB>{});
     } else {
-        if (hot_ok) pass1(std::integral_constant<int, kAlgoSW>{}, 0u);
-        if (hot_ok2) pass1(std::integral_constant<int, kAlgoSW>{}, 1u);
-        pass2(std::integral_constant<int, kAlgoSW>{});
+        if (wv == 0 && hot_ok) pass1(std::integral_constant<int, kAlgoSW>{}, 0u);
+        if (wv == 0 && hot_ok2) pass1(std::integral_constant<int, kAlgoSW>{}, 1u);
+        if (!SPLIT || wv == 1) pass2(std::integral_constant<int, kAlgoSW>{});
     }
     for (int off = 32; off > 0; off >>= 1) {
         n_allowed += __shfl_xor(n_allowed, off, 64);
@@ -1538,6 +1545,18 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
         if (n_invalid) atomicAdd(st + kStInvalid, (unsigned long long)n_invalid);
         if (n_caperr) atomicAdd(st + kStCapErr, (unsigned long long)n_caperr);
         if (n_internal) atomicOr(&a.ctl->internal_err, 1u);
+    }
+    if (SPLIT) {
+        if (wv == 1) {                                // hand over, then leave the SIMD
+            if (lane == 0) {
+                s_p2[1] = cyc_pass2; s_p2[2] = n_other;
+                __atomic_store_n(&s_p2[0], 1ULL, __ATOMIC_RELEASE);
+            }
+            return;
+        }
+        while (__atomic_load_n(&s_p2[0], __ATOMIC_ACQUIRE) == 0) __builtin_amdgcn_s_sleep(2);
+        cyc_pass2 = s_p2[1];
+        n_other = (uint32_t)s_p2[2];
     }
     // ---- write the region back, statistics
     const bool hot_touched = __any(any_hot);
@@ -1586,13 +1605,18 @@ __device__ inline void hot_chain(const RegionArgs& a, uint32_t i, RegionLds<Code
 // no occupancy that matters: one wave per SIMD gives the walk's registers room (512 VGPRs,
 // no spills).
 constexpr int kChainMinWaves = 1;
-template <class Codec, class Res, bool TOK>
-__global__ __launch_bounds__(64, kChainMinWaves) void k_hot_chains(RegionArgs a) {
+template <class Codec, class Res, bool TOK, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 128 : 64, kChainMinWaves) void k_hot_chains(RegionArgs a) {
     __shared__ RegionLds<Codec, true> S;
     const uint32_t hc = min(a.hot_count[0], kHotMax);
+    if (SPLIT) {
+        // one chain per workgroup: wave 1 leaves after its pass (the grid covers the list)
+        if (blockIdx.x < hc) hot_chain<Codec, Res, TOK, true>(a, blockIdx.x, S);
+        return;
+    }
     for (uint32_t i = blockIdx.x; i < hc; i += gridDim.x) {       // (workgroup-uniform)
         wave_fence();                                             // the last chain's LDS users
-        hot_chain<Codec, Res, TOK>(a, i, S);
+        hot_chain<Codec, Res, TOK, false>(a, i, S);
     }
 }
 
@@ -1727,12 +1751,19 @@ __global__ __launch_bounds__(256) void k_hot_fill(RegionArgs a) {
     }
 }
 
-// The chain launch: single-wave workgroups on the side stream hs.
+// The chain launch on the side stream hs: single-wave workgroups looping over the hot list,
+// or (chain_split) one two-wave workgroup per possible hot region.
 template <class Codec, class Res>
 hipError_t hot_chains_t(const RegionArgs& a, hipStream_t hs) {
+    if (a.chain_split) {
+        const dim3 g(kHotMax);
+        if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, true>), g, dim3(128), 0, hs, a);
+        else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, true>), g, dim3(128), 0, hs, a);
+        return hipGetLastError();
+    }
     const dim3 g(a.chain_grid ? min(a.chain_grid, kHotMax) : kHotMax);
-    if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true>), g, dim3(64), 0, hs, a);
-    else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false>), g, dim3(64), 0, hs, a);
+    if (a.tok) hipLaunchKernelGGL((k_hot_chains<Codec, Res, true, false>), g, dim3(64), 0, hs, a);
+    else hipLaunchKernelGGL((k_hot_chains<Codec, Res, false, false>), g, dim3(64), 0, hs, a);
     return hipGetLastError();
 }
 template <class Codec, class Res>

@@ -330,3 +330,34 @@ def test_hot_path_beside_cache_on_limiter(two_pass):
     assert st["cache_hits"] > 0, st                   # and the cache-on limiter was live
     if two_pass:
         assert st["routed"] > 0, st                   # its region was routed in pass 0
+
+
+@pytest.mark.parametrize("case", ["mixed_ops", "every_region", "two_keys", "walk_tb", "sw_limit"])
+def test_hot_chain_split(case):
+    # chain_split: a hot region's other keys (pass 2) on a second wave beside pass 1
+    tune = {"chain_split": 1, "hot_threshold": 4096}
+    kw = {}
+    if case == "mixed_ops":
+        lims = [[rl_amd.SW, 100, 10_000, 0.0], [rl_amd.TB, 20, 5_000, 3.0], [rl_amd.SW, 5, 1000, 0.0],
+                [rl_amd.TB, 500, 60_000, 50.0]]
+        tr = hot_trace(12, 1_200_000, 20_000, 0.6, [0, 1, 2, 3], 120_000, ops=0.01, hot_keys=8)
+    elif case == "every_region":
+        lims = [[rl_amd.SW, 10, 60000, 0.0], [rl_amd.TB, 50, 60000, 10.0],
+                [rl_amd.SW, 5, 1000, 0.0], [rl_amd.TB, 3, 500, 7.0]]
+        tr = trace(23, 300_000, 10_000, len(lims), 200_000, zipf=1.3, ops=0.04, invalid=0.002)
+        tune["hot_threshold"] = 1
+    elif case == "two_keys":
+        lims = [[rl_amd.TB, 50, 60000, 10.0]]
+        tr = hot_trace(17, 1_000_000, 30_000, 0.5, [0], 60_000, hot_keys=2)
+        kw["capacity"] = 1 << 17
+    elif case == "walk_tb":
+        # a dense TB key at its limit (walked) beside background keys of its region
+        lims = [[rl_amd.TB, 1000, 60000, 100.0]]
+        tr = hot_trace(18, 2_000_000, 5_000, 0.7, [0], 120_000, permits_max=2)
+        tune["walk_min"] = 0
+    else:
+        lims = [[rl_amd.SW, 1000, 60000, 0.0]]
+        tr = hot_trace(11, 1_500_000, 50_000, 0.4, [0], 180_000, permits_max=1)
+        kw["capacity"] = 1 << 17
+    got, want, _ = run(lims, tr, batches=3, tune=tune, **kw)
+    assert_same(got, want, f"chain split {case}")
