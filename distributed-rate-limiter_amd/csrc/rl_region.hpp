@@ -44,6 +44,8 @@ struct RegionLds<Codec, false> : RegionTable {};
 // Image regions keep dead slots as tombstones until live + dead slots exceed this many (of
 // 256), then drop them and relink (the sparse path rebuilds on long probe chains instead).
 constexpr uint32_t kTombCrowd = 192;
+// Token-bucket rounds: allows decided per key and round (wave_apply)
+constexpr int kTbSteps = 3;
 constexpr bool kSparseOn = true;                 // (rl_tune ablate kAblNoProbe turns it off at run time)
 
 // Sparse region (few records): the LDS table starts with every bucket kOccUnloaded and a
@@ -396,25 +398,45 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
                 ++n_rounds;
                 uint64_t sa = 0, sb = 0, sc = 0;
                 if (pending) { sa = S.sa[slot]; sb = S.sb[slot]; sc = S.sc[slot]; }
-                const int64_t last = (int64_t)sb;
-                const bool ex = (sc & 1u) && !(q.now_ms > last + L.ttl_ms);
-                const double x = __longlong_as_double((long long)sa) + (double)(q.now_ms - last) * rate;
-                const double rf = !ex ? cap : (x < cap ? x : cap);
-                const bool ok = rf >= pd;
-                const double nt = ok ? rf - pd : rf;
-                const uint64_t mut = __ballot(pending && ok) & peers;
-                const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
-                if (pending && lane <= fm) {
-                    if (lane == fm) {
-                        S.sa[slot] = (uint64_t)__double_as_longlong(nt);
-                        S.sb[slot] = (uint64_t)q.now_ms;
-                        S.sc[slot] = 1;
+                // up to kTbSteps allows per key and round: after a key's first allow (lane fm)
+                // its later pending lanes take the state that allow leaves, (tokens, now, 1),
+                // from lane fm's registers, as the next round would from the slot. The slot is
+                // written once, by the key's last allow of the round.
+                double tk = __longlong_as_double((long long)sa);
+                int64_t last = (int64_t)sb;
+                bool live = (sc & 1u) != 0;
+                bool mutated = false;                     // this lane's allow changed the state
+                uint32_t from = 0;                        // my key's lanes below it are decided
+#pragma unroll
+                for (int st = 0; st < kTbSteps; ++st) {
+                    const bool cand = pending && lane >= from;
+                    const bool ex = live && !(q.now_ms > last + L.ttl_ms);
+                    const double x = tk + (double)(q.now_ms - last) * rate;
+                    const double rf = !ex ? cap : (x < cap ? x : cap);
+                    const bool ok = rf >= pd;
+                    const double nt = ok ? rf - pd : rf;
+                    const uint64_t mut = __ballot(cand && ok) & peers;
+                    const uint32_t fm = mut ? (uint32_t)__builtin_ctzll(mut) : 64u;
+                    if (cand && lane <= fm) {
+                        mutated = lane == fm;
+                        r.alw = ok;
+                        r.rem = d2l(nt);
+                        r.tok = nt;
+                        n_allowed += ok ? 1u : 0u;
+                        pending = false;
                     }
-                    r.alw = ok;
-                    r.rem = d2l(nt);
-                    r.tok = nt;
-                    n_allowed += ok ? 1u : 0u;
-                    pending = false;
+                    if (st + 1 == kTbSteps || !__any(pending)) break;
+                    const int src = fm < 64u ? (int)fm : (int)lane;
+                    const double tk2 = __shfl(nt, src, 64);
+                    const int64_t t2 = __shfl(q.now_ms, src, 64);
+                    if (fm < 64u) { tk = tk2; last = t2; live = true; }
+                    from = fm + 1u;
+                }
+                const uint64_t mm = __ballot(mutated) & peers;
+                if (mutated && lane == 63u - (uint32_t)__builtin_clzll(mm)) {
+                    S.sa[slot] = (uint64_t)__double_as_longlong(r.tok);
+                    S.sb[slot] = (uint64_t)q.now_ms;
+                    S.sc[slot] = 1;
                 }
                 wave_fence();
             }
