@@ -75,6 +75,8 @@ struct BatchScratch {
     size_t region_cap = 0;
     uint32_t* gtile = nullptr;              // k_group*: tile_base, tile_bin, per-tile counts
     size_t gtile_cap = 0;
+    uint32_t* seg = nullptr;                // segmented pass 0: seg_adj, seg_start, seg_cnt
+    size_t seg_cap = 0;
     BatchCtl* d_ctl = nullptr;
     hipEvent_t parted = nullptr;            // pipeline: partition done (partition stream)
     hipEvent_t freed = nullptr;             // pipeline: last reader of the set done (engine stream)
@@ -125,6 +127,8 @@ struct rl_engine {
     bool region_order = true;               // rl_tune("region_order"): largest regions dispatched first
     uint32_t order_prefix = 4096;           // rl_tune("order_prefix"): ... after this many of the smallest
     uint32_t tile_items = 0;                // rl_tune("tile_items"): partition tile rounds (0: auto)
+    uint32_t segments = 1;                  // rl_tune("segments"): two-pass batches' pass-0 output
+                                            // in that many tile segments ([segment][bin])
     uint32_t group_bits = 12;               // rl_tune("group_bits"): two-pass batches' pass-0
                                             // high digit (2^12 bins + the routed ones)
     uint32_t* order = nullptr;              // [order_cap + 1]
@@ -339,7 +343,7 @@ extern "C" void rl_destroy(rl_engine* e) {
         dfree(B.rec0); dfree(B.rec1); dfree(B.pos0); dfree(B.pos1); dfree(B.res); dfree(B.tok);
         dfree(B.ext); dfree(B.digit);
         dfree(B.counts); dfree(B.bin_total); dfree(B.bin_base);
-        dfree(B.region_count); dfree(B.region_start); dfree(B.gtile);
+        dfree(B.region_count); dfree(B.region_start); dfree(B.gtile); dfree(B.seg);
         dfree(B.d_ctl);
         if (B.parted) (void)hipEventDestroy(B.parted);
         if (B.freed) (void)hipEventDestroy(B.freed);
@@ -650,6 +654,9 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     const bool route = hot_on && e->route && passes == 2 &&
                        (1u << dh) + kRouteBins <= (1u << kMaxDigitBits);
     const uint32_t nb0 = route ? (1u << dh) + kRouteBins : 1u << dh;
+    // segmented pass-0 output (two passes): n_segs runs of seg_tiles tiles
+    const uint32_t seg_tiles = passes == 2 && e->segments > 1 ? (nt + e->segments - 1) / e->segments : nt;
+    const uint32_t n_segs = (nt + seg_tiles - 1) / seg_tiles;
     // Scratch set and partition stream. With RL_OPT_PIPELINE the partition (stages 1-3)
     // runs on e->pstream into one of two scratch sets, so batch k+1's partition overlaps
     // batch k's region stage; the region stage and the unpermute stay on e->stream (state
@@ -725,6 +732,19 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     mark_on(e, ps, 1);
     HIP_OK(launch_scan_rows(B.counts, B.counts, nb0, nt, B.bin_total, ps));
     HIP_OK(launch_scan_small(B.bin_total, B.bin_base, nb0, ps));
+    if (n_segs > 1) {
+        const size_t words = (size_t)3 * nb0 * n_segs;
+        if (words > B.seg_cap) {
+            if (e->pipeline) { HIP_OK(hipStreamSynchronize(s)); HIP_OK(hipStreamSynchronize(ps)); }
+            dfree(B.seg);
+            if (dalloc(&B.seg, words) != RL_OK) { B.seg_cap = 0; return RL_E_NOMEM; }
+            B.seg_cap = words;
+        }
+        const size_t m = (size_t)nb0 * n_segs;
+        HIP_OK(launch_seg_base(B.counts, B.bin_total, B.bin_base, nb0, 1u << dh, nt, seg_tiles, n_segs,
+                               B.seg, B.seg + m, B.seg + 2 * m, ps));
+        pa.seg_adj = B.seg; pa.n_segs = n_segs; pa.seg_tiles = seg_tiles;
+    }
     mark_on(e, ps, 2);
     HIP_OK(launch_scatter(pa, true, wide, ps));
     if (route)
@@ -748,8 +768,9 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ga.tile_recs = group_tile_recs((uint32_t)s0);
         ga.pad = (uint32_t)n;
         ga.ablate = e->ablate;
-        ga.max_tiles = (uint32_t)((n + ga.tile_recs - 1) / ga.tile_recs) + ga.n_bins0;
-        const size_t words = (size_t)ga.n_bins0 + 1 + (size_t)ga.max_tiles * (1 + ((size_t)1 << s0));
+        ga.max_tiles = (uint32_t)((n + ga.tile_recs - 1) / ga.tile_recs) + ga.n_bins0 * n_segs;
+        const size_t words = (size_t)ga.n_bins0 + 1 + (size_t)ga.max_tiles * (1 + ((size_t)1 << s0)) +
+                             (n_segs > 1 ? (size_t)2 * ga.max_tiles : 0);
         if (words > B.gtile_cap) {
             if (e->pipeline) { HIP_OK(hipStreamSynchronize(s)); HIP_OK(hipStreamSynchronize(ps)); }
             dfree(B.gtile);
@@ -759,6 +780,12 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
         ga.tile_base = B.gtile;
         ga.tile_bin = B.gtile + ga.n_bins0 + 1;
         ga.tcount = ga.tile_bin + ga.max_tiles;
+        if (n_segs > 1) {
+            const size_t m = (size_t)nb0 * n_segs;
+            ga.seg_start = B.seg + m; ga.seg_cnt = B.seg + 2 * m; ga.n_segs = n_segs;
+            ga.tile_beg = ga.tcount + (size_t)ga.max_tiles * ((size_t)1 << s0);
+            ga.tile_end = ga.tile_beg + ga.max_tiles;
+        }
         HIP_OK(launch_group(ga, wide, ps));
         rstart = B.region_start;
         rcount = nullptr;
@@ -1194,6 +1221,11 @@ extern "C" int rl_tune(rl_engine* e, const char* key, int64_t value) {
     if (std::strcmp(key, "tile_items") == 0) {        // partition tile = value x 512 requests
         if (value != 0 && (value < 8 || value > 1024 || value % 8 != 0)) return RL_E_INVALID_ARG;
         e->tile_items = (uint32_t)value;
+        return RL_OK;
+    }
+    if (std::strcmp(key, "segments") == 0) {          // two-pass batches: pass-0 output segments
+        if (value < 1 || value > 64) return RL_E_INVALID_ARG;
+        e->segments = (uint32_t)value;
         return RL_OK;
     }
     if (std::strcmp(key, "group_bits") == 0) {        // two-pass batches: pass-0 high-digit bits

@@ -193,6 +193,11 @@ __device__ inline uint32_t tile_at(uint32_t it, uint32_t n_tiles) {
     return it * gridDim.x + xcd_remap(blockIdx.x, gridDim.x);
 }
 
+// A pass-0 tile's cursor base for bin b (added to the row prefix counts[b][tile]).
+__device__ inline uint32_t cursor_base(const PartArgs& a, uint32_t b, uint32_t tile) {
+    return a.seg_adj ? a.seg_adj[b * a.n_segs + tile / a.seg_tiles] : a.bin_base[b];
+}
+
 // Global bin id of element i (pass 0: raw arrays; later passes: records).
 template <class Codec, bool RAW>
 __device__ inline uint32_t bin_of(const PartArgs& a, uint32_t i, const LimLds& L) {

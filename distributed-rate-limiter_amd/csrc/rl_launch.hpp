@@ -81,6 +81,12 @@ struct PartArgs {
     uint32_t sc_split;         // rl_tune("scatter_split"): loads and stores in separate waves
     uint32_t* counts;          // [bins][n_tiles]: per-tile histogram, then exclusive row scan
     const uint32_t* bin_base;  // [bins]
+    // Segmented output (two-pass batches, rl_tune "segments" > 1; nullable): the tiles cut into
+    // n_segs runs of seg_tiles, the normal bins laid out [segment][bin] so that the write
+    // fronts of all bins stay inside one segment's part of the array at a time; a tile's
+    // cursor base is seg_adj[bin * n_segs + tile / seg_tiles] instead of bin_base[bin]
+    const uint32_t* seg_adj;
+    uint32_t n_segs, seg_tiles;
     BatchCtl* ctl;
     uint32_t ablate;           // rl_tune("ablate"): measurement-only variants (0 = product)
     uint32_t n_bins_pass;      // bins of this pass (0: 1 << digit_bits)
@@ -251,6 +257,13 @@ struct GroupArgs {
     uint32_t* tile_base;       // [n_bins0 + 1] first tile of each bin; [n_bins0] = tiles
     uint32_t* tile_bin;        // [max_tiles] bin of each tile
     uint32_t* tcount;          // [max_tiles][2^s0] per-tile region counts, then cursors
+    // segmented pass 0 (nullable): bin b's records in n_segs runs, [seg_start, + seg_cnt)
+    // (b * n_segs + s); tiles then never cross a run: tile_beg / tile_end [max_tiles]
+    const uint32_t* seg_start;
+    const uint32_t* seg_cnt;
+    uint32_t n_segs;
+    uint32_t* tile_beg;
+    uint32_t* tile_end;
     uint32_t pad;              // the batch size: rec_out / pos_out hold 64 padding entries past it
     uint32_t ablate;           // rl_tune("ablate") (measurement only)
 };
@@ -376,6 +389,12 @@ hipError_t launch_group(const GroupArgs& a, bool wide, hipStream_t s);
 // Routing: after the pass-0 scan, copy the routed bins' ranges (before pass 1 reuses the scan
 // arrays) and set ctl->n_normal; after the hot selection, list the routed regions first; after
 // the batch's hot preparation, the next batch's route list (largest listed regions >= thr).
+// Segmented pass 0: from the row-scanned counts, each (bin, segment)'s start in the
+// pass-0 array (normal bins segment-major, routed bins bin-major as before) and count.
+hipError_t launch_seg_base(const uint32_t* counts, const uint32_t* bin_total,
+                           const uint32_t* bin_base, uint32_t bins, uint32_t lo_bins,
+                           uint32_t n_tiles, uint32_t seg_tiles, uint32_t n_segs,
+                           uint32_t* seg_adj, uint32_t* seg_start, uint32_t* seg_cnt, hipStream_t s);
 hipError_t launch_route_ranges(const uint32_t* route_list, const uint32_t* bin_base,
                                const uint32_t* bin_total, uint32_t lo_bins, uint32_t* route_start,
                                uint32_t* route_cnt, BatchCtl* ctl, hipStream_t s);

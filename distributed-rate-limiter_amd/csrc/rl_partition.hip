@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kTileThreads) void k_scatter(PartArgs a) {
         if (tile0 >= n) continue;                        // (workgroup-uniform)
         __syncthreads();     // previous tile's LDS users are done
         for (uint32_t b = t; b < bins; b += kTileThreads) {
-            cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
+            cur[b] = cursor_base(a, b, tile) + a.counts[(size_t)b * a.n_tiles + tile];
             cntw[b] = 0;
         }
         // kScatterDepth rounds of inputs in flight; out-of-range lanes re-load element n-1
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(2 * kTileThreads) void k_scatter_split(PartArgs a) 
         if (loader) {
             ScatterIn<Codec, RAW> in[kSplitDepth];
             for (uint32_t b = lt; b < bins; b += kTileThreads)
-                cur[b] = a.bin_base[b] + a.counts[(size_t)b * a.n_tiles + tile];
+                cur[b] = cursor_base(a, b, tile) + a.counts[(size_t)b * a.n_tiles + tile];
 #pragma unroll
             for (int k = 0; k < kSplitDepth; ++k) in[k].load(a, min(tile0 + (uint32_t)k * kTileThreads + lt, last));
             Rec r0;
@@ -525,15 +525,36 @@ __global__ __launch_bounds__(1024) void k_gtiles(GroupArgs a) {
     const uint32_t t = threadIdx.x, nb = a.n_bins0, T = a.tile_recs;
     const uint32_t per = (nb + 1023) / 1024;
     const uint32_t b0 = min(t * per, nb), b1 = min(b0 + per, nb);
+    const uint32_t S = a.seg_start ? a.n_segs : 1u;
+    // (segmented: a bin's runs in segment order, tiles never crossing a run)
+    auto run_of = [&](uint32_t b, uint32_t s, uint32_t& st, uint32_t& c) {
+        if (a.seg_start) { st = a.seg_start[b * S + s]; c = a.seg_cnt[b * S + s]; }
+        else { st = a.bin_base[b]; c = a.bin_total[b]; }
+    };
     uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += (a.bin_total[b] + T - 1) / T;
+    for (uint32_t b = b0; b < b1; ++b)
+        for (uint32_t s = 0; s < S; ++s) {
+            uint32_t st, c;
+            run_of(b, s, st, c);
+            sum += (c + T - 1) / T;
+        }
     uint32_t tot;
     uint32_t base = block_exclusive_scan<1024>(sum, tmp, &tot);
     for (uint32_t b = b0; b < b1; ++b) {
-        const uint32_t nt = (a.bin_total[b] + T - 1) / T;
-        a.tile_base[b] = base;
-        for (uint32_t j = 0; j < nt && base + j < a.max_tiles; ++j) a.tile_bin[base + j] = b;
-        base += nt;
+        a.tile_base[b] = min(base, a.max_tiles);
+        for (uint32_t s = 0; s < S; ++s) {
+            uint32_t st, c;
+            run_of(b, s, st, c);
+            const uint32_t nt = (c + T - 1) / T;
+            for (uint32_t j = 0; j < nt && base + j < a.max_tiles; ++j) {
+                a.tile_bin[base + j] = b;
+                if (a.seg_start) {
+                    a.tile_beg[base + j] = st + j * T;
+                    a.tile_end[base + j] = st + min((j + 1) * T, c);
+                }
+            }
+            base += nt;
+        }
     }
     if (t == 0) a.tile_base[nb] = min(tot, a.max_tiles);
 }
@@ -542,6 +563,11 @@ __global__ __launch_bounds__(1024) void k_gtiles(GroupArgs a) {
 __device__ inline void group_tile(const GroupArgs& a, uint32_t t, uint32_t& b, uint32_t& beg,
                                   uint32_t& end) {
     b = a.tile_bin[t];
+    if (a.seg_start) {
+        beg = a.tile_beg[t];
+        end = a.tile_end[t];
+        return;
+    }
     const uint32_t j = t - a.tile_base[b];
     const uint32_t bb = a.bin_base[b], be = bb + a.bin_total[b];
     beg = bb + j * a.tile_recs;
@@ -814,6 +840,60 @@ __global__ __launch_bounds__(kGPThreads) void k_gplace_lds(GroupArgs a) {
             }
         }
     }
+}
+
+// ------------------------------------------------------------------ segmented pass 0
+// From the row-scanned counts (exclusive prefix per bin over the tiles): each (bin, segment)
+// run's count, its start — normal bins segment-major over [0, n_normal), routed bins
+// bin-major after them, exactly where the unsegmented layout put them — and the cursor
+// base a tile of that segment adds to its row prefix (seg_adj = start - prefix at the
+// segment's first tile; modular arithmetic).
+__global__ __launch_bounds__(1024) void k_seg_base(const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ bin_total,
+                                                   const uint32_t* __restrict__ bin_base,
+                                                   uint32_t bins, uint32_t lo, uint32_t nt,
+                                                   uint32_t seg_tiles, uint32_t S, uint32_t* seg_adj,
+                                                   uint32_t* seg_start, uint32_t* seg_cnt) {
+    __shared__ uint32_t tmp[16];
+    auto pre = [&](uint32_t b, uint32_t s) -> uint32_t {
+        const uint32_t t0 = s * seg_tiles;
+        return t0 < nt ? counts[(size_t)b * nt + t0] : bin_total[b];
+    };
+    const uint32_t N = S * lo;
+    const uint32_t per = (N + 1023) / 1024;
+    const uint32_t i0 = min(threadIdx.x * per, N), i1 = min(i0 + per, N);
+    uint32_t sum = 0;
+    for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t s = i / lo, b = i % lo;
+        sum += pre(b, s + 1) - pre(b, s);
+    }
+    uint32_t run = block_exclusive_scan<1024>(sum, tmp, nullptr);
+    for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t s = i / lo, b = i % lo;
+        const uint32_t p0 = pre(b, s), c = pre(b, s + 1) - p0;
+        seg_start[b * S + s] = run;
+        seg_cnt[b * S + s] = c;
+        seg_adj[b * S + s] = run - p0;
+        run += c;
+    }
+    for (uint32_t b = lo + threadIdx.x; b < bins; b += 1024)
+        for (uint32_t s = 0; s < S; ++s) {
+            const uint32_t p0 = pre(b, s);
+            seg_adj[b * S + s] = bin_base[b];
+            seg_start[b * S + s] = bin_base[b] + p0;
+            seg_cnt[b * S + s] = pre(b, s + 1) - p0;
+        }
+}
+
+hipError_t launch_seg_base(const uint32_t* counts, const uint32_t* bin_total,
+                           const uint32_t* bin_base, uint32_t bins, uint32_t lo_bins,
+                           uint32_t n_tiles, uint32_t seg_tiles, uint32_t n_segs,
+                           uint32_t* seg_adj, uint32_t* seg_start, uint32_t* seg_cnt, hipStream_t s) {
+    if (seg_tiles == 0 || (size_t)(n_segs - 1) * seg_tiles >= n_tiles || lo_bins > bins)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_seg_base, dim3(1), dim3(1024), 0, s, counts, bin_total, bin_base, bins,
+                       lo_bins, n_tiles, seg_tiles, n_segs, seg_adj, seg_start, seg_cnt);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ routing helpers

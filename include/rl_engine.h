@@ -234,7 +234,8 @@ int  rl_sync(rl_engine* e);
  * walk, default 1), "walk_min" (keys walked: at least this many allows expected per batch,
  * default 4000), "chain_split" (hot chains as two-wave workgroups, default 0), "group_bits"
  * (two-pass batches: bits of the pass-0 digit, default 12; the local grouping resolves the
- * rest), "tile_items" (partition tile = value x 512 requests; 0 = by batch size), "sparse_max",
+ * rest), "segments" (two-pass batches: pass-0 output in that many tile segments, default 1),
+ * "tile_items" (partition tile = value x 512 requests; 0 = by batch size), "sparse_max",
  * "stage_timing", "debug_regions" and the "*_per_cu" grid sizes.
  * Every setting gives the same decisions. "fail_batches" = k makes the next k batch
  * calls fail with RL_E_DEVICE before enqueuing anything (tests of callers' error paths). */

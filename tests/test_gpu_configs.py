@@ -189,6 +189,14 @@ def test_config_sw_zipf_routed_batches():
     assert all(s["routed"] > (1 << 26) for s in stats[1:]), [s["routed"] for s in stats]
 
 
+@pytest.mark.parametrize("segs", [8, 16])
+def test_config_sw_zipf_segmented(segs):
+    """The headline's routed whole batches with the pass-0 output segmented
+    (rl_tune "segments"): bins laid out [segment][bin], grouped from their runs."""
+    stats = run_stream("sw_zipf", 2, tune=(("segments", segs),))
+    assert stats[1]["routed"] > (1 << 26)
+
+
 @pytest.mark.timeout(600)
 def test_config_zipf_1b_steady_state():
     """configs[4]'s per-GPU share over four consecutive whole bench batches (routing on)."""

@@ -180,6 +180,26 @@ def test_hot_routed_two_pass(algo, route):
     assert_same(got, want, f"routed {algo} route={route}")
 
 
+@pytest.mark.parametrize("segs", [3, 16])
+@pytest.mark.parametrize("algo", ["sw", "tb"])
+def test_hot_routed_two_pass_segmented(algo, segs):
+    # the pass-0 output in segments ([segment][bin]; 16 > the batch's 7 tiles: one per tile)
+    lims = ([[rl_amd.SW, 200, 20_000, 0.0], [rl_amd.SW, 5, 1000, 0.0]] if algo == "sw" else
+            [[rl_amd.TB, 50, 60_000, 10.0], [rl_amd.TB, 20, 5_000, 3.0]])
+    tr = hot_trace(31, 2_000_000, 300_000, 0.5, [0, 1], 100_000, ops=0.005, hot_keys=6)
+    tr[1][::997] = 0
+    got, want, _ = run(lims, tr, batches=5, capacity=1 << 22,
+                       tune={"hot_threshold": 8192, "segments": segs})
+    assert_same(got, want, f"segmented {algo} segs={segs}")
+
+
+def test_hot_routed_every_region_segmented():
+    lims = [[rl_amd.SW, 50, 30_000, 0.0], [rl_amd.TB, 40, 30_000, 8.0]]
+    tr = trace(33, 1_200_000, 400_000, 2, 150_000, zipf=1.2, ops=0.02, invalid=0.001)
+    got, want, _ = run(lims, tr, batches=4, capacity=1 << 22, tune={"hot_threshold": 1, "segments": 4})
+    assert_same(got, want, "routed every region segmented")
+
+
 def test_hot_routed_shifting_hot_set():
     # the hot keys change every batch: regions routed because of the previous batch are
     # small (or empty) in this one and still go through the chains
