@@ -267,23 +267,10 @@ __global__ __launch_bounds__(64) void k_hot_prep(RegionArgs a) {
 // other record, for the second key those of neither (the records wave 1 applies). Group
 // words: the same over the group's chunks, with 0/1 flags for the counts. The wave keeps
 // four chunks' records in flight.
-__device__ inline uint64_t wave_min64(uint64_t v) {
-    for (int o = 32; o > 0; o >>= 1) { const uint64_t x = __shfl_xor(v, o, 64); v = x < v ? x : v; }
-    return v;
-}
-__device__ inline uint64_t wave_max64(uint64_t v) {
-    for (int o = 32; o > 0; o >>= 1) { const uint64_t x = __shfl_xor(v, o, 64); v = x > v ? x : v; }
-    return v;
-}
-
-__device__ inline uint32_t wave_min32(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) { const uint32_t x = __shfl_xor(v, o, 64); v = x < v ? x : v; }
-    return v;
-}
-__device__ inline uint32_t wave_max32(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) { const uint32_t x = __shfl_xor(v, o, 64); v = x > v ? x : v; }
-    return v;
-}
+__device__ inline uint64_t wave_min64(uint64_t v) { return wave_min_dpp<uint64_t>(v); }
+__device__ inline uint64_t wave_max64(uint64_t v) { return wave_max_dpp<uint64_t>(v); }
+__device__ inline uint32_t wave_min32(uint32_t v) { return wave_min_dpp<uint32_t>(v); }
+__device__ inline uint32_t wave_max32(uint32_t v) { return wave_max_dpp<uint32_t>(v); }
 
 // A key the walk pays for, from its expected allows e (an upper estimate: TB a full bucket plus
 // the refill over the batch's span; SW the limit per window over the windows the span

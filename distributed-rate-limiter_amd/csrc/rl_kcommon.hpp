@@ -247,6 +247,47 @@ __device__ inline uint32_t pass_digit(const PartArgs& a, uint32_t g, const Route
 
 // first probe position of a key inside its region (4-slot aligned: probing reads buckets)
 __device__ inline uint32_t slot_home(uint64_t h) { return (uint32_t)h & (kRegionSlots - 4); }
+// Wave-wide min / max with every lane active: DPP inside each 16-lane row (xor 1, xor 2, half
+// mirror, mirror: each an ALU op reading a neighbour's register), then the four rows' results
+// by readlane; uniform result. (__shfl_xor lowers to ds_bpermute: six dependent LDS round
+// trips per reduction, twelve for 64 bits.)
+template <int C>
+__device__ inline uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, C, 0xF, 0xF, false);
+}
+template <int C>
+__device__ inline uint64_t dpp64(uint64_t v) {
+    return (uint64_t)dpp32<C>((uint32_t)v) | ((uint64_t)dpp32<C>((uint32_t)(v >> 32)) << 32);
+}
+template <class T, class Op>
+__device__ inline T wave_reduce_dpp(T v, Op op) {
+    if constexpr (sizeof(T) == 8) {
+        v = op(v, (T)dpp64<0xB1>((uint64_t)v));      // quad_perm(1,0,3,2): lane ^ 1
+        v = op(v, (T)dpp64<0x4E>((uint64_t)v));      // quad_perm(2,3,0,1): lane ^ 2
+        v = op(v, (T)dpp64<0x141>((uint64_t)v));     // row_half_mirror: 8-lane groups
+        v = op(v, (T)dpp64<0x140>((uint64_t)v));     // row_mirror: 16-lane rows
+        const uint64_t u = (uint64_t)v;
+        auto rl = [&](int l) {
+            return (T)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l) << 32));
+        };
+        return op(op(rl(0), rl(16)), op(rl(32), rl(48)));
+    } else {
+        v = op(v, (T)dpp32<0xB1>((uint32_t)v));
+        v = op(v, (T)dpp32<0x4E>((uint32_t)v));
+        v = op(v, (T)dpp32<0x141>((uint32_t)v));
+        v = op(v, (T)dpp32<0x140>((uint32_t)v));
+        auto rl = [&](int l) { return (T)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l); };
+        return op(op(rl(0), rl(16)), op(rl(32), rl(48)));
+    }
+}
+template <class T> __device__ inline T wave_min_dpp(T v) {
+    return wave_reduce_dpp(v, [](T x, T y) { return y < x ? y : x; });
+}
+template <class T> __device__ inline T wave_max_dpp(T v) {
+    return wave_reduce_dpp(v, [](T x, T y) { return y > x ? y : x; });
+}
+
 __device__ inline void wave_fence() { __builtin_amdgcn_wave_barrier(); asm volatile("" ::: "memory"); }
 
 static inline uint32_t tiles_for(uint32_t n) { return (n + kTile - 1) / kTile; }

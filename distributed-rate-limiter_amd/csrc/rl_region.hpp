@@ -276,11 +276,7 @@ __device__ inline Applied wave_apply(const RegionArgs& a, LdsT& S, const DevLimi
         }
         if (slot >= 0) geo = sw_geo_ref(q.now_ms, L, sp.wref);
         // window index relative to the wave's first window (2 bits; 3 = "far")
-        int64_t wmin = slot >= 0 ? geo.curr_start : INT64_MAX;
-        for (int o = 32; o > 0; o >>= 1) {
-            const int64_t x = __shfl_xor(wmin, o, 64);
-            wmin = x < wmin ? x : wmin;
-        }
+        const int64_t wmin = wave_min_dpp<int64_t>(slot >= 0 ? geo.curr_start : INT64_MAX);
         // (window starts are multiples of w: compares instead of a 64-bit division)
         const int64_t dw = geo.curr_start - wmin, w1 = L.window_ms;
         const int64_t wi = slot < 0 ? 3 : dw == 0 ? 0 : dw == w1 ? 1 : dw == 2 * w1 ? 2 : 3;
