@@ -718,7 +718,10 @@ static int run_batch_device(rl_engine* e, size_t n, const uint64_t* key, const i
     pa.n = (uint32_t)n; pa.n_tiles = nt; pa.tile_items = titems; pa.n_lim = (uint32_t)e->lims.size();
     pa.shard_bits = e->shard_bits; pa.lims = e->d_lims; pa.ctl = B.d_ctl;
     pa.counts = B.counts; pa.bin_base = B.bin_base; pa.ablate = e->ablate;
-    pa.up_per_cu = e->up_per_cu; pa.sc_per_cu = e->sc_per_cu; pa.sc_split = e->sc_split;
+    // (128K-request tiles: one upsweep tile per workgroup, 8 per CU: upsweep0 0.76 -> 0.73 ms on
+    // sw_zipf over 6 runs, run_r06ab.sh)
+    pa.up_per_cu = e->up_per_cu ? e->up_per_cu : (titems > (uint32_t)kTileItems ? 8u : 0u);
+    pa.sc_per_cu = e->sc_per_cu; pa.sc_split = e->sc_split;
     // ---- pass 0 (the high digit: region >> s0) from the caller's arrays; routed hot
     // regions get bins 2^dh + slot and their records go straight to the final array (rec1)
     pa.digit_shift = s0; pa.digit_bits = route ? ceil_log2(nb0) : dh;
