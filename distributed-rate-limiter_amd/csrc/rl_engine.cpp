@@ -114,7 +114,7 @@ struct rl_engine {
     uint32_t walk_hint = 0;                 // listed regions that wanted a walk in the last batch
                                             // seen complete (walk_tab is allocated once it is > 0)
     uint32_t walk_min = kWalkMinAllows;     // rl_tune("walk_min"): fewest expected allows walked
-    bool chain_split = false;               // rl_tune("chain_split"): two-wave hot chains
+    bool chain_split = true;                // rl_tune("chain_split"): two-wave hot chains
     uint32_t* hot_mark = nullptr;           // [hot_mark_cap] epoch marks per bin
     size_t hot_mark_cap = 0;
     uint32_t epoch = 0;

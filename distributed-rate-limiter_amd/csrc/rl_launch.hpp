@@ -143,7 +143,7 @@ struct RegionArgs {
     // region order[g]; order[n_regions] = number of non-empty regions listed)
     const uint32_t* order;
     uint32_t order_prefix;     // that many of the smallest regions are dispatched first
-    uint32_t chain_split;      // chains as two-wave workgroups (pass 2 beside pass 1)
+    uint32_t chain_split;      // chains as two-wave workgroups (pass 2 beside pass 1; default)
     uint32_t chain_grid;       // workgroups of the chain launch (each loops over the hot list
                                // with that stride): sized on the host from an earlier batch's
                                // hot count, so a batch with no hot region launches few idle ones

@@ -232,7 +232,7 @@ int  rl_sync(rl_engine* e);
  * tables: the previous batch's hot regions skip the second partition pass, default 1),
  * "region_order" (largest regions dispatched first, default 1), "walk" (the hot chains' allow
  * walk, default 1), "walk_min" (keys walked: at least this many allows expected per batch,
- * default 4000), "chain_split" (hot chains as two-wave workgroups, default 0), "group_bits"
+ * default 4000), "chain_split" (hot chains as two-wave workgroups, default 1), "group_bits"
  * (two-pass batches: bits of the pass-0 digit, default 12; the local grouping resolves the
  * rest), "segments" (two-pass batches: pass-0 output in that many tile segments, default 1),
  * "tile_items" (partition tile = value x 512 requests; 0 = by batch size), "sparse_max",

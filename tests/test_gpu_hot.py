@@ -319,6 +319,7 @@ def test_hot_chain_launch_smaller_than_hot_list():
     e = rl_amd.Engine(max_batch=1 << 22, capacity=1 << 14)
     for l in lims:
         e.add_limiter(*l)
+    e.tune("chain_split", 0)                  # (two-wave chains launch one workgroup per entry)
     o = COracle(lims)
     cut = 200_000
     got = [[], [], []]
@@ -354,8 +355,9 @@ def test_hot_path_beside_cache_on_limiter(two_pass):
 
 @pytest.mark.parametrize("case", ["mixed_ops", "every_region", "two_keys", "walk_tb", "sw_limit"])
 def test_hot_chain_split(case):
-    # chain_split: a hot region's other keys (pass 2) on a second wave beside pass 1
-    tune = {"chain_split": 1, "hot_threshold": 4096}
+    # chain_split off (one wave per chain, pass 2 after pass 1); on is the default every other
+    # hot test runs
+    tune = {"chain_split": 0, "hot_threshold": 4096}
     kw = {}
     if case == "mixed_ops":
         lims = [[rl_amd.SW, 100, 10_000, 0.0], [rl_amd.TB, 20, 5_000, 3.0], [rl_amd.SW, 5, 1000, 0.0],
